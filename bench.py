@@ -1,0 +1,295 @@
+"""bench.py — device-resident WebSocket unmask throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU, RCCL)
+
+A step = one websocketframeBatchDecodeDevice call over the whole synthetic batch
+(BASELINE.json configs[1]: 1,048,576 masked binary frames x 4 KiB payload, split
+into rx segments of 16 frames = 65,536 connections), in place, inputs resident
+in HBM. value = payload GiB/s over all ranks (weak scaling: every rank decodes
+its own full batch; frames are independent, no collective in the data path —
+RCCL only carries the max-over-ranks time). Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+class Workload:
+    """A synthetic batch laid out in HBM exactly as a reactor would hand it over:
+    frames back to back in one buffer, rx segments of `fps` frames each."""
+
+    CONFIGS = {
+        # name: nframes, plen_kind, fixed_len, b0_kind, seed, frames per segment
+        "cfg1": (16, 0, 125, 1, 1, 16),
+        "cfg2": (1 << 20, 0, 4096, 0, 2, 16),
+        "cfg3": (1 << 20, 1, 0, 0, 3, 16),
+        "cfg4": (1 << 20, 0, 65536, 0, 4, 16),   # per GPU: 8M x 64 KiB over 8 GPUs
+        "cfg5": (1 << 22, 0, 1024, 2, 5, 16),    # 256K messages x 16 fragments
+    }
+    DESCRIPTION = {
+        "cfg1": "16 masked text frames x 125 B",
+        "cfg2": "1M masked binary frames x 4 KiB, 16-frame rx segments",
+        "cfg3": "1M frames, payload uniform from {125 B, 1500 B, 64 KiB}, 16-frame rx segments",
+        "cfg4": "1M masked binary frames x 64 KiB per GPU (8M over 8 GPUs)",
+        "cfg5": "256K messages x 16 continuation frames x 1 KiB (16-frame segments = messages)",
+    }
+
+    @classmethod
+    def make(cls, name, dev, nframes=None, seed_offset=0):
+        from util_amd import synth
+        n, pk, fl, bk, seed, fps = cls.CONFIGS[name]
+        if nframes is not None:
+            n = nframes
+        return cls(name, dev, n, pk, fl, bk, seed + seed_offset, fps, synth)
+
+    def __init__(self, name, dev, n, pk, fl, bk, seed, fps, gen):
+        import torch
+        from util_amd import wsframe as W
+        self.torch, self.W = torch, W
+        self.name, self.dev, self.nframes, self.plen_kind, self.fixed_len = name, dev, n, pk, fl
+        self.b0_kind, self.seed, self.fps = bk, seed, fps
+        plen = gen.plens(pk, fl, seed, n)
+        wl = gen.wirelens(plen)
+        off = np.zeros(n, dtype=np.uint64)
+        off[1:] = np.cumsum(wl[:-1], dtype=np.uint64)
+        self.plen_h, self.wirelen_h, self.off_h = plen, wl, off
+        self.wire_bytes = int(wl.sum())
+        self.payload_bytes = int(plen.sum())
+        self.nseg = (n + fps - 1) // fps
+        seg_off = off[::fps]
+        seg_end = np.append(seg_off[1:], np.uint64(self.wire_bytes))
+        self.seg_off_h, self.seg_len_h = seg_off, seg_end - seg_off
+        t = torch
+        self.buf = t.empty(self.wire_bytes + 256, dtype=t.uint8, device=dev)
+        self.frame_off = t.from_numpy(off.astype(np.int64)).to(dev)
+        self.seg_off = t.from_numpy(seg_off.astype(np.int64)).to(dev)
+        self.seg_len = t.from_numpy(self.seg_len_h.astype(np.int64)).to(dev)
+        self.desc = t.empty(self.nseg * fps * 32, dtype=t.uint8, device=dev)
+        self.res = t.empty(self.nseg * 16, dtype=t.uint8, device=dev)
+        self.buf[self.wire_bytes:].zero_()
+        W.synth_device(self.buf, self.frame_off, n, pk, fl, bk, seed)
+        self.decodes = 0
+
+    # algorithmic HBM bytes of one decode: read every wire byte, write every payload byte
+    @property
+    def algo_bytes(self):
+        return self.wire_bytes + self.payload_bytes
+
+    def decode(self, stream=None):
+        self.W.batch_decode_device(self.buf, self.seg_off, self.seg_len, self.fps, self.desc, self.res, stream=stream)
+        self.decodes += 1
+
+    def verify(self, expect_plain):
+        t = self.torch
+        mm = t.zeros(1, dtype=t.int64, device=self.dev)
+        self.W.synth_verify_device(self.buf, self.frame_off, self.nframes, self.plen_kind, self.fixed_len, self.seed,
+                                   expect_plain, mm)
+        t.cuda.synchronize()
+        return int(mm.item())
+
+    def check_descs(self):
+        """descriptors of every frame equal what websocketframeDecode returns for the generator's frames"""
+        t = self.torch
+        d = self.desc.view(t.int64).view(-1, 4)
+        fo, do, dl, rest = d[:, 0], d[:, 1], d[:, 2], d[:, 3]
+        plen = t.from_numpy(self.plen_h.astype(np.int64)).to(self.dev)
+        wl = t.from_numpy(self.wirelen_h.astype(np.int64)).to(self.dev)
+        hl = wl - plen
+        n = self.nframes
+        assert t.equal(fo[:n], self.frame_off)
+        assert t.equal(do[:n], self.frame_off + hl)
+        assert t.equal(dl[:n], plen)
+        ret = rest[:n] & 0xFFFFFFFF
+        assert t.equal(ret, wl)
+        flags = (rest[:n] >> 32) & 0xFFFFFFFF
+        f = t.arange(n, device=self.dev)
+        if self.b0_kind == 2:
+            j = f & 15
+            fin = (j == 15).long()
+            typ = t.where(j == 0, 2, 0)
+        else:
+            fin = t.ones_like(f)
+            typ = t.full_like(f, 1 if self.b0_kind == 1 else 2)
+        exp = fin | (typ << 8) | (1 << 16) | (hl << 24)
+        assert t.equal(flags, exp)
+
+    def host_sample(self, nframes):
+        """copy the first `nframes` frames' wire bytes (as currently in HBM) to host memory"""
+        nseg = max(1, nframes // self.fps)
+        end = int(self.seg_off_h[nseg]) if nseg < self.nseg else self.wire_bytes
+        return (self.buf[:end].cpu().numpy().copy(), self.seg_off_h[:nseg].copy(), self.seg_len_h[:nseg].copy(),
+                int(self.plen_h[: nseg * self.fps].sum()))
+
+    def free(self):
+        del self.buf, self.desc, self.res
+        self.torch.cuda.empty_cache()
+
+
+def cpu_baseline(sample, threads, min_seconds=1.0):
+    """time the reference's own websocketframeDecode (oracle/_ref, reactor loop driver) —
+    or the oracle restatement when the reference build is absent — on host cores"""
+    buf, so, sl, payload = sample
+    ref = os.path.join(REPO, "oracle", "_ref", "libwsref_loop.so")
+    if os.path.exists(ref):
+        lib = C.CDLL(ref)
+        fn = lib.ref_decode_segments
+        fn.restype = C.c_ulonglong
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]
+        kind = "reference"
+
+        def run(lo, hi):
+            nf = C.c_ulonglong()
+            fn(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo, C.byref(nf))
+    else:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from oracle_lib import load_oracle
+        from util_amd.wsframe import DESC_DTYPE, SEGRES_DTYPE
+        lib = load_oracle()
+        kind = "port"
+
+        def run(lo, hi):
+            d = np.empty((hi - lo) * 16, DESC_DTYPE)
+            r = np.empty(hi - lo, SEGRES_DTYPE)
+            lib.ws_oracle_decode_segments(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo, 16,
+                                          None, d.ctypes.data, r.ctypes.data)
+    nseg = len(so)
+
+    def timed(nthreads, passes):
+        bounds = np.linspace(0, nseg, nthreads + 1).astype(int)
+
+        def worker(i):
+            for _ in range(passes):
+                run(bounds[i], bounds[i + 1])
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(nthreads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0
+
+    # calibrate passes so the multi-thread run lasts about min_seconds of wall time
+    t1 = timed(1, 1)
+    single = payload / t1 / 2**30
+    passes = max(2, int(min_seconds / max(1e-6, t1 / threads)))
+    passes += passes % 2  # even: buffer returns to its masked state
+    tn = timed(threads, passes)
+    multi = payload * passes / tn / 2**30
+    return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "single_thread_gibs": round(single, 3),
+            "cpu_seconds": round(tn * threads + t1, 2),
+            "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %d passes x %d threads, "
+                      "reactor loop net_reactor.c:515-526 over websocketframeDecode" %
+                      (nseg * 16, nseg, payload / 2**20, passes, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    wl = Workload.make(args.config, dev, seed_offset=rank)
+    torch.cuda.synchronize()
+    sample = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sample = wl.host_sample(65536)
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        wl.decode()
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        wl.decode()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # correctness of the timed run: after an odd number of decodes the buffer holds plaintext
+    mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
+    if world > 1:
+        mt = torch.tensor([mism], dtype=torch.int64, device=dev)
+        dist.all_reduce(mt)
+        mism = int(mt.item())
+
+    payload_all = wl.payload_bytes * world * args.steps
+    value = payload_all / elapsed / 2**30
+    mean_kern = float(kern_ms.mean()) / 1e3
+    achieved = wl.algo_bytes / mean_kern / 1e9
+    out = {
+        "metric": "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
+        "config": {"workload": Workload.DESCRIPTION[args.config], "config": args.config,
+                   "frames_per_gpu": wl.nframes, "frames_per_segment": wl.fps, "segments_per_gpu": wl.nseg,
+                   "wire_bytes_per_gpu": wl.wire_bytes, "payload_bytes_per_gpu": wl.payload_bytes,
+                   "parallelism": "frame-range shards, %d independent GPU(s)" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "kernel": "ws_decode_segments_kernel", "algo_bytes_per_launch": wl.algo_bytes,
+                     "kernel_ms_mean": round(mean_kern * 1e3, 4), "kernel_ms_min": round(float(kern_ms.min()), 4)},
+        "verified": mism == 0,
+        "cpu_baseline": None,
+    }
+    if sample is not None:
+        out["cpu_baseline"] = cpu_baseline(sample, min(args.cpu_threads, os.cpu_count() or 1))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if mism:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * wsframe_amd.h — C ABI of the MI355X WebSocket frame-decode engine
+ * (libwsframe_amd.so). Drop-in for hujianzhe/util crt/protocol/websocketframe.
+ *
+ * Part 1 re-exports the eight reference symbols with identical signatures and
+ * semantics (inc/crt/protocol/websocketframe.h:42-49). They work on host
+ * memory, one frame / one handshake at a time, exactly like the reference, so
+ * existing callers (user glue behind NetChannelExProc_t.on_decode,
+ * inc/component/net_channel_ex.h:22-27) link unchanged.
+ *
+ * Part 2 is the batch API the GPU path adds: a device-resident
+ * batch of rx segments (one per connection inbuf, src/component/net_reactor.c
+ * :465-545) is decoded by hand-written gfx950 kernels with the exact semantics
+ * of the reactor's per-frame loop (net_reactor.c:515-526) running
+ * websocketframeDecode (websocketframe.c:112-165) on every segment.
+ *
+ * Plain pointers and sizes only; no torch types. Every pointer named d_* is
+ * device memory, h_* is host memory. Buffers are owned by the caller; the
+ * library never frees user memory.
+ */
+#ifndef UTIL_AMD_WSFRAME_AMD_H
+#define UTIL_AMD_WSFRAME_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSFRAME_AMD_EXPORT __attribute__((visibility("default")))
+
+/* ---- Part 1: reference ABI (websocketframe.h:10-19, :42-49) ---------------- */
+
+enum {
+    WEBSOCKET_CONTINUE_FRAME = 0,
+    WEBSOCKET_TEXT_FRAME = 1,
+    WEBSOCKET_BINARY_FRAME = 2,
+    WEBSOCKET_CLOSE_FRAME = 8,
+    WEBSOCKET_PING_FRAME = 9,
+    WEBSOCKET_PONG_FRAME = 10
+};
+
+#define WEBSOCKET_MAX_ENCODE_HEADLENGTH 10
+
+/* websocketframe.c:16-32 */
+WSFRAME_AMD_EXPORT char* websocketframeComputeSecAccept(const char* sec_key, unsigned int sec_keylen,
+                                                        char sec_accept[60]);
+/* websocketframe.c:34-73 */
+WSFRAME_AMD_EXPORT int websocketframeDecodeHandshakeRequest(const char* data, unsigned int datalen,
+                                                            const char** sec_key, unsigned int* sec_keylen,
+                                                            const char** sec_protocol,
+                                                            unsigned int* sec_protocol_len);
+/* websocketframe.c:75-84 */
+WSFRAME_AMD_EXPORT char* websocketframeEncodeHandshakeResponse(const char* sec_accept,
+                                                               unsigned int sec_accept_len, char buf[162]);
+/* websocketframe.c:86-108 */
+WSFRAME_AMD_EXPORT char* websocketframeEncodeHandshakeResponseWithProtocol(const char* sec_accept_key,
+                                                                           unsigned int sec_accept_len,
+                                                                           const char* sec_protocol,
+                                                                           unsigned int sec_protocol_len);
+/* websocketframe.c:110 */
+WSFRAME_AMD_EXPORT void websocketframeFreeString(char* s);
+/* websocketframe.c:112-165 */
+WSFRAME_AMD_EXPORT int websocketframeDecode(unsigned char* buf, unsigned long long len, unsigned char** data,
+                                            unsigned long long* datalen, int* is_fin, int* type);
+/* websocketframe.c:167-174 */
+WSFRAME_AMD_EXPORT unsigned int websocketframeEncodeHeadLength(unsigned long long datalen);
+/* websocketframe.c:176-202 */
+WSFRAME_AMD_EXPORT void websocketframeEncode(void* headbuf, int is_fin, int prev_is_fin, int type,
+                                             unsigned long long datalen);
+
+/* ---- Part 2: batch decode on MI355X ------------------------------------------ */
+
+/* Per-frame result: the four out-params of websocketframeDecode plus its
+ * return value and the frame's position. 32 bytes, naturally aligned. */
+typedef struct WebsocketFrameDesc_t {
+    unsigned long long frame_off; /* wire offset of the frame from the batch buffer base */
+    unsigned long long data_off;  /* payload offset from the buffer base; ~0ULL where *data == NULL */
+    unsigned long long datalen;   /* *datalen */
+    int ret;                      /* websocketframeDecode return value (never 0 in a descriptor) */
+    unsigned char is_fin;         /* *is_fin */
+    unsigned char type;           /* *type (raw 4-bit opcode, not validated, as the reference) */
+    unsigned char masked;         /* MASK bit of byte 1 */
+    unsigned char hdrlen;         /* 2 + ext + mask bytes */
+} WebsocketFrameDesc_t;
+
+#define WEBSOCKET_DATA_OFF_NULL (~0ULL)
+
+/* Segment stop reasons (WebsocketSegResult_t.status) */
+enum {
+    WEBSOCKET_SEG_OK = 0,              /* consumed everything, or stopped at an incomplete tail (ret 0) */
+    WEBSOCKET_SEG_MAX_FRAMES = 1,      /* descriptor capacity reached; resubmit from `consumed` */
+    WEBSOCKET_SEG_ERR_DECODE = -1,     /* a frame returned ret < 0 (int truncation, websocketframe.c:164):
+                                          the reactor marks the channel invalid (net_reactor.c:518-520) */
+    WEBSOCKET_SEG_ERR_LEN_WRAP = -2    /* masked frame whose u64 length sum wraps (websocketframe.c:149):
+                                          the reference would unmask past the buffer (undefined behaviour);
+                                          fenced off here, nothing is written for that frame */
+};
+
+/* Per-segment result. 16 bytes. */
+typedef struct WebsocketSegResult_t {
+    unsigned long long consumed; /* Σ ret of decoded frames = bytes the reactor would drop from inbuf */
+    unsigned int n_frames;       /* descriptors written for this segment */
+    int status;                  /* WEBSOCKET_SEG_* */
+} WebsocketSegResult_t;
+
+/* Decode a device-resident batch of rx segments in place, asynchronously on
+ * `hip_stream` (hipStream_t, NULL = default stream).
+ *   d_buf          batch buffer (device); payloads are unmasked in place
+ *   d_seg_off/len  nseg segments [off, off+len) of d_buf (device arrays); must not overlap
+ *   max_frames     descriptor capacity per segment (>= 1)
+ *   d_desc_base    optional (device, may be NULL): first descriptor slot of segment s;
+ *                  NULL means s * max_frames
+ *   d_desc         descriptor array (device)
+ *   d_res          nseg segment results (device)
+ * Semantics: for every segment, bit-identical to running
+ *   off = 0; while (off < len) { r = websocketframeDecode(buf+off, len-off, ...);
+ *                                if (r < 0) error; if (r == 0) break; off += r; }
+ * (net_reactor.c:515-526), including every reference quirk (§SURVEY 4).
+ * Returns 0, or a negative code if the launch failed (see websocketframeGpuLastError). */
+WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, const unsigned long long* d_seg_off,
+                                                       const unsigned long long* d_seg_len, unsigned int nseg,
+                                                       unsigned int max_frames,
+                                                       const unsigned long long* d_desc_base,
+                                                       WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
+                                                       void* hip_stream);
+
+/* Same, but buffers live in host memory (the reactor's m_inbuf): pinned
+ * staging, H2D, kernel, D2H, synchronous. Segment offsets are relative to h_buf.
+ * h_desc must hold nseg*max_frames descriptors (desc_base form not offered). */
+WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
+                                                     const unsigned long long* h_seg_off,
+                                                     const unsigned long long* h_seg_len, unsigned int nseg,
+                                                     unsigned int max_frames, WebsocketFrameDesc_t* h_desc,
+                                                     WebsocketSegResult_t* h_res, int device);
+
+/* Last HIP error string of the calling thread's most recent failed call ("" if none). */
+WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
+
+/* ---- Part 3: synthetic batches (bench / test input only, not the decode path) - */
+
+/* Fill d_buf with nframes masked frames generated by util_amd/csrc/ws_synth.h.
+ * d_frame_off[f] = wire offset of frame f (device, exclusive prefix sum of
+ * ws_synth_wirelen). plen_kind/b0_kind: WS_PLEN_* / WS_B0_* of ws_synth.h. */
+WSFRAME_AMD_EXPORT int websocketframeSynthDevice(unsigned char* d_buf, const unsigned long long* d_frame_off,
+                                                 unsigned long long nframes, int plen_kind,
+                                                 unsigned long long fixed_len, int b0_kind,
+                                                 unsigned long long seed, void* hip_stream);
+
+/* Count bytes of decoded payloads that differ from the generator's plaintext
+ * (size-independent full-batch check). Adds into *d_mismatch (device u64). */
+WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned char* d_buf,
+                                                       const unsigned long long* d_frame_off,
+                                                       unsigned long long nframes, int plen_kind,
+                                                       unsigned long long fixed_len, unsigned long long seed,
+                                                       int expect_plain, unsigned long long* d_mismatch,
+                                                       void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

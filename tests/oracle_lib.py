@@ -1,0 +1,56 @@
+"""ctypes binding of the oracle (oracle/libws_oracle.so) — test infrastructure only."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(REPO, "oracle", "libws_oracle.so")
+_lib = None
+
+
+def load_oracle():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE):
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+        lib = C.CDLL(ORACLE)
+        vp, u64, i32, u32 = C.c_void_p, C.c_ulonglong, C.c_int, C.c_uint
+        P = C.POINTER
+        lib.ws_oracle_decode.restype = i32
+        lib.ws_oracle_decode.argtypes = [vp, u64, P(vp), P(u64), P(i32), P(i32)]
+        lib.ws_oracle_encode_headlen.restype = u32
+        lib.ws_oracle_encode_headlen.argtypes = [u64]
+        lib.ws_oracle_encode.argtypes = [vp, i32, i32, i32, u64]
+        lib.ws_oracle_decode_segments.restype = None
+        lib.ws_oracle_decode_segments.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp]
+        lib.ws_oracle_sec_accept.restype = vp
+        lib.ws_oracle_sec_accept.argtypes = [C.c_char_p, u32, vp]
+        _lib = lib
+    return _lib
+
+
+def oracle_segments(buf, seg_off, seg_len, max_frames, desc_base=None):
+    """run the a5 loop oracle; buf (numpy uint8) modified in place. Returns (desc, res)."""
+    from util_amd.wsframe import DESC_DTYPE, SEGRES_DTYPE
+    lib = load_oracle()
+    nseg = len(seg_off)
+    so = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    sl = np.ascontiguousarray(seg_len, dtype=np.uint64)
+    nslots = int(max(desc_base) + max_frames) if desc_base is not None and nseg else nseg * max_frames
+    desc = np.zeros(max(1, nslots), dtype=DESC_DTYPE)
+    res = np.zeros(max(1, nseg), dtype=SEGRES_DTYPE)
+    db = None if desc_base is None else np.ascontiguousarray(desc_base, dtype=np.uint64)
+    lib.ws_oracle_decode_segments(buf.ctypes.data, so.ctypes.data, sl.ctypes.data, nseg, max_frames,
+                                  None if db is None else db.ctypes.data, desc.ctypes.data, res.ctypes.data)
+    return desc, res[:nseg]
+
+
+def used_descs(desc, res, max_frames, desc_base=None):
+    """concatenate the used descriptor slots of every segment"""
+    out = []
+    for s in range(len(res)):
+        b = int(desc_base[s]) if desc_base is not None else s * max_frames
+        out.append(desc[b:b + int(res[s]["n_frames"])])
+    return np.concatenate(out) if out else desc[:0]

@@ -1,0 +1,129 @@
+"""C-ABI checks that need no GPU: libwsframe_amd.so loads, exports every symbol
+include/wsframe_amd.h declares, and its host half (the eight reference symbols)
+matches the reference's golden vectors. No compute call touches a GPU here."""
+import ctypes as C
+import hashlib
+import os
+import re
+import subprocess
+
+import numpy as np
+
+import util_amd
+from util_amd import _lib
+from util_amd import wsframe as W
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "wsframe_amd.h")).read()
+    return sorted(set(re.findall(r"WSFRAME_AMD_EXPORT[^;]*?\b(websocketframe\w+)\s*\(", src, re.S)))
+
+
+def test_exports_every_declared_symbol():
+    util_amd.load_lib()
+    declared = header_symbols()
+    assert len(declared) == 13
+    assert sorted(_lib.EXPORTS) == declared
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (websocketframe\w+)", out))
+    assert set(declared) <= exported, set(declared) - exported
+    lib = util_amd.load_lib()
+    for s in declared:
+        assert getattr(lib, s) is not None
+
+
+def test_reference_signature_set():
+    """the eight reference symbols (websocketframe.h:42-49) are all there"""
+    ref8 = {"websocketframeComputeSecAccept", "websocketframeDecodeHandshakeRequest",
+            "websocketframeEncodeHandshakeResponse", "websocketframeEncodeHandshakeResponseWithProtocol",
+            "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
+            "websocketframeEncode"}
+    assert ref8 <= set(header_symbols())
+
+
+def test_host_decode_single(golden):
+    for c in golden("decode_single.json"):
+        wire = bytes.fromhex(c["input"])
+        buf = bytearray(wire if wire else b"\0")
+        r, doff, dl, fin, typ = W.websocketframeDecode(buf, c["len"])
+        assert r == c["ret"], c["name"]
+        if c["data_off"] == "untouched":
+            assert doff is None and dl is None, c["name"]
+        else:
+            assert (doff, dl, fin, typ) == (c["data_off"], c["datalen"], c["fin"], c["type"]), c["name"]
+        assert hashlib.sha256(bytes(buf[: len(wire)])).hexdigest() == c["output_sha256"], c["name"]
+
+
+def test_host_decode_loop_segments(golden):
+    """the host symbol driven by the reactor loop reproduces the segment fixtures"""
+    for c in golden("decode_segments.json"):
+        buf = bytearray(bytes.fromhex(c["input"]))
+        for so, sl, sg in zip(c["seg_off"], c["seg_len"], c["segments"]):
+            off, nf, frames = 0, 0, []
+            while off < sl and nf < c["max_frames"]:
+                r, doff, dl, fin, typ = W.websocketframeDecode(buf, sl - off, so + off)
+                if r == 0:
+                    break
+                frames.append((r, doff, dl, fin, typ))
+                nf += 1
+                if r < 0:
+                    break
+                off += r & 0xFFFFFFFF
+            exp = [(f["ret"], f["data_off"], f["datalen"], f["fin"], f["type"]) for f in sg["frames"]]
+            if sg["status"] == -2:
+                continue
+            assert frames == exp, c["name"]
+            assert off == sg["consumed"], c["name"]
+        assert hashlib.sha256(bytes(buf)).hexdigest() == c["output_sha256"], c["name"]
+
+
+def test_host_encode(golden):
+    for c in golden("handshake.json")["encode_header"]:
+        assert W.websocketframeEncodeHeadLength(c["datalen"]) == c["headlen"]
+        assert W.websocketframeEncode(c["is_fin"], c["prev_is_fin"], c["type"], c["datalen"]).hex() == c["head"]
+
+
+def test_host_handshake(golden):
+    hs = golden("handshake.json")
+    for c in hs["sec_accept"]:
+        assert W.websocketframeComputeSecAccept(c["key"].encode()) == c["accept"], c["key"]
+    assert W.websocketframeComputeSecAccept(b"dGhlIHNhbXBsZSBub25jZQ==") == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo="
+    for c in hs["decode_request"]:
+        got = W.websocketframeDecodeHandshakeRequest(c["request"].encode())
+        exp = (c["ret"], c["sec_key_off"], c["sec_key_len"], c["sec_protocol_off"], c["sec_protocol_len"])
+        assert got == exp, c["request"]
+    for c in hs["encode_response"]:
+        assert W.websocketframeEncodeHandshakeResponse(c["accept"].encode()) == c["response"]
+        proto = None if c["protocol"] is None else c["protocol"].encode()
+        assert W.websocketframeEncodeHandshakeResponseWithProtocol(c["accept"].encode(), proto) == \
+            c["response_with_protocol"]
+
+
+def test_struct_layout():
+    assert C.sizeof(_lib.WsDesc) == 32 and C.sizeof(_lib.WsSegRes) == 16
+    assert W.DESC_DTYPE.itemsize == 32
+    assert np.dtype(W.SEGRES_DTYPE).itemsize == 16
+
+
+def test_host_decode_word_xor_matches_bytewise():
+    """host unmask (8-byte words) vs a byte loop at every alignment and length"""
+    rng = np.random.default_rng(1)
+    for align in range(8):
+        for plen in (0, 1, 7, 8, 9, 15, 16, 17, 125, 126, 300, 4096, 65536, 70001):
+            key = rng.integers(0, 256, 4, dtype=np.uint8)
+            pay = rng.integers(0, 256, plen, dtype=np.uint8)
+            hl = 2 if plen < 126 else (4 if plen <= 0xFFFF else 10)
+            h = bytearray([0x82])
+            if hl == 2:
+                h.append(0x80 | plen)
+            elif hl == 4:
+                h += bytes([0x80 | 126]) + plen.to_bytes(2, "big")
+            else:
+                h += bytes([0x80 | 127]) + plen.to_bytes(8, "big")
+            frame = bytes(h) + key.tobytes() + (pay ^ np.resize(key, plen)).tobytes()
+            buf = bytearray(align) + bytearray(frame)
+            r, doff, dl, fin, typ = W.websocketframeDecode(buf, len(frame), align)
+            assert r == len(frame) and dl == plen
+            assert bytes(buf[align + hl + 4:]) == pay.tobytes()

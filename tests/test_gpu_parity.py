@@ -1,0 +1,222 @@
+"""GPU parity: websocketframeBatchDecodeDevice (gfx950 kernels, through the C ABI)
+against the oracle (oracle/ws_oracle.c, pinned to the reference) and the
+reference's golden vectors. Bit-exact: buffer bytes, descriptors, segment results.
+Full-size configs are checked by size-independent properties (decode restores
+the generator's plaintext; decoding twice restores the wire bytes)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import wsynth
+from oracle_lib import oracle_segments, used_descs
+from util_amd import wsframe as W
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):
+    """copy to device (with slack), decode, copy back. Returns (buf, desc, res)."""
+    n = len(host_buf)
+    d = torch.zeros(n + pad, dtype=torch.uint8, device=dev)
+    if n:
+        d[:n] = torch.from_numpy(host_buf).to(dev)
+    so = torch.tensor(np.asarray(seg_off, dtype=np.int64), device=dev)
+    sl = torch.tensor(np.asarray(seg_len, dtype=np.int64), device=dev)
+    nseg = len(seg_off)
+    nslots = int(max(desc_base) + max_frames) if desc_base is not None and nseg else nseg * max_frames
+    desc = torch.full((max(1, nslots) * 32,), 0xEE, dtype=torch.uint8, device=dev)
+    res = torch.full((max(1, nseg) * 16,), 0xEE, dtype=torch.uint8, device=dev)
+    db = None if desc_base is None else torch.tensor(np.asarray(desc_base, dtype=np.int64), device=dev)
+    W.batch_decode_device(d, so, sl, max_frames, desc, res, desc_base=db)
+    torch.cuda.synchronize()
+    out = d.cpu().numpy()
+    assert not out[n:].any(), "kernel wrote past the batch"
+    return out[:n], desc.cpu().numpy().view(W.DESC_DTYPE), res.cpu().numpy().view(W.SEGRES_DTYPE)[:nseg]
+
+
+def assert_same(dev, wire, seg_off, seg_len, max_frames, desc_base=None, tag=""):
+    gb, gd, gr = gpu_decode(dev, wire.copy(), seg_off, seg_len, max_frames, desc_base)
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, seg_off, seg_len, max_frames, desc_base)
+    assert np.array_equal(gr, orr), tag
+    assert np.array_equal(used_descs(gd, gr, max_frames, desc_base), used_descs(od, orr, max_frames, desc_base)), tag
+    if not np.array_equal(gb, ob):
+        bad = np.nonzero(gb != ob)[0]
+        raise AssertionError("%s: %d bytes differ, first at %d" % (tag, len(bad), bad[0]))
+    return gb, gd, gr
+
+
+def test_golden_segments(dev, golden):
+    for c in golden("decode_segments.json"):
+        wire = np.frombuffer(bytes.fromhex(c["input"]), dtype=np.uint8).copy()
+        gb, gd, gr = gpu_decode(dev, wire, c["seg_off"], c["seg_len"], c["max_frames"])
+        assert hashlib.sha256(gb.tobytes()).hexdigest() == c["output_sha256"], c["name"]
+        assert [int(x) for x in gr["consumed"]] == [s["consumed"] for s in c["segments"]], c["name"]
+        assert [int(x) for x in gr["status"]] == [s["status"] for s in c["segments"]], c["name"]
+        assert_same(dev, wire, c["seg_off"], c["seg_len"], c["max_frames"], tag=c["name"])
+
+
+def test_golden_single_frames_as_segments(dev, golden):
+    """every single-frame fixture whose buffer is real (len <= bytes) as one segment"""
+    cases = [c for c in golden("decode_single.json") if c["len"] <= len(c["input"]) // 2]
+    blob, so, sl = bytearray(), [], []
+    for c in cases:
+        blob += bytes((len(blob) * 7 + 5) % 13 + 1)  # odd gaps -> every alignment
+        so.append(len(blob))
+        sl.append(c["len"])
+        blob += bytes.fromhex(c["input"])
+    wire = np.frombuffer(bytes(blob), dtype=np.uint8).copy()
+    gb, gd, gr = gpu_decode(dev, wire, so, sl, 1)
+    for i, c in enumerate(cases):
+        seg = gb[so[i]:so[i] + len(c["input"]) // 2]
+        assert hashlib.sha256(seg.tobytes()).hexdigest() == c["output_sha256"], c["name"]
+        if c["ret"] != 0:
+            d = gd[i]
+            assert int(gr[i]["n_frames"]) == 1, c["name"]
+            assert int(d["ret"]) == c["ret"] and int(d["datalen"]) == c["datalen"], c["name"]
+            assert (int(d["is_fin"]), int(d["type"])) == (c["fin"], c["type"]), c["name"]
+            exp_off = W.DATA_OFF_NULL if c["data_off"] is None else so[i] + c["data_off"]
+            assert int(d["data_off"]) == exp_off, c["name"]
+        else:
+            assert int(gr[i]["n_frames"]) == 0 and int(gr[i]["consumed"]) == 0, c["name"]
+
+
+@pytest.mark.parametrize("idx", range(4))
+def test_golden_seeded_batches(dev, golden, idx):
+    c = golden("batches.json")[idx]
+    wire, off, pl, plain = wsynth.make_batch(c["nframes"], c["plen_kind"], c["fixed_len"], c["b0_kind"], c["seed"])
+    fps, n = c["frames_per_segment"], c["nframes"]
+    seg_off = [int(off[i]) for i in range(0, n, fps)]
+    ends = [int(off[i + fps]) if i + fps < n else len(wire) for i in range(0, n, fps)]
+    seg_len = [e - s for s, e in zip(seg_off, ends)]
+    gb, gd, gr = gpu_decode(dev, wire.copy(), seg_off, seg_len, fps)
+    assert hashlib.sha256(gb.tobytes()).hexdigest() == c["output_sha256"]
+    assert hashlib.sha256(used_descs(gd, gr, fps).tobytes()).hexdigest() == c["desc_sha256"]
+
+
+def random_stream(rng, nseg, max_frame=5000):
+    blob, so, sl = bytearray(), [], []
+    for _ in range(nseg):
+        blob += bytes(int(rng.integers(0, 20)))
+        so.append(len(blob))
+        parts = []
+        for _ in range(int(rng.integers(0, 12))):
+            plen = int(rng.choice([0, 1, 2, 3, 5, 15, 16, 17, 31, 33, 125, 126, 127, 1000, 1023, 4096,
+                                   int(rng.integers(0, max_frame))]))
+            key = rng.integers(0, 256, 4, dtype=np.uint8) if rng.random() < 0.85 else None
+            form = 7 if plen < 126 else (16 if plen <= 0xFFFF else 64)
+            if plen < 126 and rng.random() < 0.1:
+                form = 16
+            if plen <= 0xFFFF and rng.random() < 0.05:
+                form = 64
+            h = bytearray([int(rng.integers(0, 256))])
+            m = 0x80 if key is not None else 0
+            if form == 7:
+                h.append(m | plen)
+            elif form == 16:
+                h += bytes([m | 126]) + plen.to_bytes(2, "big")
+            else:
+                h += bytes([m | 127]) + plen.to_bytes(8, "big")
+            if key is not None:
+                h += key.tobytes()
+            parts.append(bytes(h) + rng.integers(0, 256, plen, dtype=np.uint8).tobytes())
+        seg = b"".join(parts)
+        r = rng.random()
+        if r < 0.3 and seg:
+            seg = seg[: int(rng.integers(0, len(seg) + 1))]
+        elif r < 0.4:
+            seg += rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+        blob += seg
+        sl.append(len(seg))
+    return np.frombuffer(bytes(blob), dtype=np.uint8).copy(), so, sl
+
+
+@pytest.mark.parametrize("seed,max_frames", [(1, 16), (2, 3), (3, 1), (4, 64)])
+def test_random_streams_vs_oracle(dev, seed, max_frames):
+    rng = np.random.default_rng(seed)
+    wire, so, sl = random_stream(rng, 3000)
+    assert_same(dev, wire, so, sl, max_frames, tag="seed%d" % seed)
+
+
+def test_desc_base_and_empty_segments(dev):
+    rng = np.random.default_rng(11)
+    wire, so, sl = random_stream(rng, 500)
+    sl = [0 if i % 7 == 0 else x for i, x in enumerate(sl)]
+    base = np.cumsum([0] + [8] * (len(so) - 1)).astype(np.int64)[::-1].copy()  # reversed slots
+    assert_same(dev, wire, so, sl, 8, desc_base=base, tag="desc_base")
+
+
+def test_garbage_streams(dev):
+    rng = np.random.default_rng(12)
+    n = 1 << 20
+    wire = rng.integers(0, 256, n, dtype=np.uint8)
+    cuts = np.sort(rng.choice(n, 4000, replace=False))
+    so = [int(x) for x in cuts[:-1]]
+    sl = [int(b - a) for a, b in zip(cuts[:-1], cuts[1:])]
+    assert_same(dev, wire, so, sl, 32, tag="garbage")
+
+
+def test_large_frames_unaligned(dev):
+    """64 KiB+ payloads at every 16-B phase, and a few MiB-sized frames"""
+    blob, so, sl = bytearray(), [], []
+    rng = np.random.default_rng(3)
+    for phase in range(16):
+        for plen in (65535, 65536, 65537, 3 << 20):
+            blob += bytes(phase + 1)
+            key = rng.integers(0, 256, 4, dtype=np.uint8)
+            if plen <= 0xFFFF:
+                h = bytes([0x82, 0x80 | 126]) + plen.to_bytes(2, "big")
+            else:
+                h = bytes([0x82, 0x80 | 127]) + plen.to_bytes(8, "big")
+            f = h + key.tobytes() + rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+            so.append(len(blob))
+            sl.append(len(f))
+            blob += f
+    wire = np.frombuffer(bytes(blob), dtype=np.uint8).copy()
+    assert_same(dev, wire, so, sl, 2, tag="large")
+
+
+def test_synth_matches_numpy_generator(dev):
+    for (n, pk, fl, bk, seed) in [(40, wsynth.PLEN_FIXED, 4096, wsynth.B0_BINARY, 9),
+                                  (30, wsynth.PLEN_MIX3, 0, wsynth.B0_BINARY, 10),
+                                  (32, wsynth.PLEN_FIXED, 1024, wsynth.B0_FRAG16, 11),
+                                  (16, wsynth.PLEN_FIXED, 125, wsynth.B0_TEXT, 1)]:
+        wire, off, pl, plain = wsynth.make_batch(n, pk, fl, bk, seed)
+        d = torch.zeros(len(wire), dtype=torch.uint8, device=dev)
+        offs = torch.tensor(off.astype(np.int64), device=dev)
+        W.synth_device(d, offs, n, pk, fl, bk, seed)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), wire)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
+def test_full_size_properties(dev, cfg):
+    """BASELINE configs at full size: decode -> generator plaintext; decode again -> wire bytes;
+    descriptors/segment results consistent with the generator's lengths"""
+    import bench
+    wl = bench.Workload.make(cfg, dev)
+    try:
+        wl.decode()
+        torch.cuda.synchronize()
+        assert wl.verify(expect_plain=True) == 0
+        res = wl.res.view(torch.int64).view(-1, 2)
+        assert int(res[:, 0].sum()) == wl.wire_bytes
+        nf = (res[:, 1] & 0xFFFFFFFF)
+        st = (res[:, 1] >> 32)
+        assert int(nf.sum()) == wl.nframes and int((st != 0).sum()) == 0
+        wl.check_descs()
+        wl.decode()
+        torch.cuda.synchronize()
+        assert wl.verify(expect_plain=False) == 0
+    finally:
+        wl.free()

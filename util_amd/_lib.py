@@ -1,0 +1,85 @@
+"""Locate, build and load libwsframe_amd.so (in-tree, next to this file).
+
+Fails loudly: there is no Python or CPU fallback for the batch path.
+"""
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libwsframe_amd.so")
+_lib = None
+
+
+class WsDesc(C.Structure):
+    _fields_ = [("frame_off", C.c_ulonglong), ("data_off", C.c_ulonglong), ("datalen", C.c_ulonglong),
+                ("ret", C.c_int), ("is_fin", C.c_ubyte), ("type", C.c_ubyte), ("masked", C.c_ubyte),
+                ("hdrlen", C.c_ubyte)]
+
+
+class WsSegRes(C.Structure):
+    _fields_ = [("consumed", C.c_ulonglong), ("n_frames", C.c_uint), ("status", C.c_int)]
+
+
+# every symbol include/wsframe_amd.h declares
+EXPORTS = [
+    "websocketframeComputeSecAccept", "websocketframeDecodeHandshakeRequest",
+    "websocketframeEncodeHandshakeResponse", "websocketframeEncodeHandshakeResponseWithProtocol",
+    "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
+    "websocketframeEncode", "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
+    "websocketframeGpuLastError", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
+]
+
+
+def build_lib(force=False):
+    """make -C util_amd/csrc (hipcc --offload-arch=gfx950 + gcc)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc")] + (["-B"] if force else []), check=True)
+    return LIB_PATH
+
+
+def load_lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libwsframe_amd.so not built: run __graft_entry__.build() "
+                           "(make -C util_amd/csrc); there is no fallback path")
+    lib = C.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = C.c_void_p, C.c_ulonglong, C.c_uint, C.c_int
+    P = C.POINTER
+    lib.websocketframeDecode.restype = i32
+    lib.websocketframeDecode.argtypes = [vp, u64, P(vp), P(u64), P(i32), P(i32)]
+    lib.websocketframeEncodeHeadLength.restype = u32
+    lib.websocketframeEncodeHeadLength.argtypes = [u64]
+    lib.websocketframeEncode.restype = None
+    lib.websocketframeEncode.argtypes = [vp, i32, i32, i32, u64]
+    lib.websocketframeComputeSecAccept.restype = vp
+    lib.websocketframeComputeSecAccept.argtypes = [C.c_char_p, u32, vp]
+    lib.websocketframeDecodeHandshakeRequest.restype = i32
+    lib.websocketframeDecodeHandshakeRequest.argtypes = [vp, u32, P(vp), P(u32), P(vp), P(u32)]
+    lib.websocketframeEncodeHandshakeResponse.restype = vp
+    lib.websocketframeEncodeHandshakeResponse.argtypes = [C.c_char_p, u32, vp]
+    lib.websocketframeEncodeHandshakeResponseWithProtocol.restype = vp
+    lib.websocketframeEncodeHandshakeResponseWithProtocol.argtypes = [C.c_char_p, u32, C.c_char_p, u32]
+    lib.websocketframeFreeString.restype = None
+    lib.websocketframeFreeString.argtypes = [vp]
+    lib.websocketframeBatchDecodeDevice.restype = i32
+    lib.websocketframeBatchDecodeDevice.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp]
+    lib.websocketframeBatchDecodeHost.restype = i32
+    lib.websocketframeBatchDecodeHost.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, i32]
+    lib.websocketframeGpuLastError.restype = C.c_char_p
+    lib.websocketframeGpuLastError.argtypes = []
+    lib.websocketframeSynthDevice.restype = i32
+    lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
+    lib.websocketframeSynthVerifyDevice.restype = i32
+    lib.websocketframeSynthVerifyDevice.argtypes = [vp, vp, u64, i32, u64, u64, i32, vp, vp]
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        err = load_lib().websocketframeGpuLastError().decode(errors="replace")
+        raise RuntimeError("%s failed (%d): %s" % (what, rc, err))

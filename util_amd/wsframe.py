@@ -1,0 +1,161 @@
+"""Python mirror of the websocketframe API (inc/crt/protocol/websocketframe.h:10-49)
+and of the batch API (include/wsframe_amd.h Part 2), over libwsframe_amd.so.
+
+Host functions take a mutable ``bytearray``/numpy uint8 buffer and behave like
+the C functions (same argument meaning, same return conventions: >0 bytes
+consumed, 0 incomplete, <0 error). Batch functions take torch CUDA tensors and
+only pass raw device pointers and the current HIP stream to the C ABI.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import WsDesc, WsSegRes, check, load_lib
+
+WEBSOCKET_CONTINUE_FRAME = 0
+WEBSOCKET_TEXT_FRAME = 1
+WEBSOCKET_BINARY_FRAME = 2
+WEBSOCKET_CLOSE_FRAME = 8
+WEBSOCKET_PING_FRAME = 9
+WEBSOCKET_PONG_FRAME = 10
+WEBSOCKET_MAX_ENCODE_HEADLENGTH = 10
+
+SEG_OK, SEG_MAX_FRAMES, SEG_ERR_DECODE, SEG_ERR_LEN_WRAP = 0, 1, -1, -2
+DATA_OFF_NULL = 0xFFFFFFFFFFFFFFFF
+
+DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("data_off", "<u8"), ("datalen", "<u8"), ("ret", "<i4"),
+                       ("is_fin", "u1"), ("type", "u1"), ("masked", "u1"), ("hdrlen", "u1")])
+SEGRES_DTYPE = np.dtype([("consumed", "<u8"), ("n_frames", "<u4"), ("status", "<i4")])
+assert DESC_DTYPE.itemsize == C.sizeof(WsDesc) == 32
+assert SEGRES_DTYPE.itemsize == C.sizeof(WsSegRes) == 16
+
+
+def _addr(buf):
+    """address of a writable host buffer (bytearray or numpy array)"""
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    return C.addressof((C.c_char * len(buf)).from_buffer(buf))
+
+
+# ------------------------------------------------------------------ host, one frame
+
+def websocketframeDecode(buf, length=None, offset=0):
+    """websocketframe.c:112-165 on buf[offset:offset+length], in place.
+
+    Returns (ret, data_off, datalen, is_fin, type); data_off is the payload offset
+    into ``buf`` (None where the C function sets *data = NULL). Out-params the C
+    function leaves untouched (ret 0) come back as None.
+    """
+    lib = load_lib()
+    if length is None:
+        length = len(buf) - offset
+    sent = 0xA5A5A5A5A5A5A5A5
+    data, datalen, fin, typ = C.c_void_p(sent), C.c_ulonglong(sent), C.c_int(-7), C.c_int(-7)
+    base = _addr(buf) if len(buf) else 0
+    r = lib.websocketframeDecode(base + offset, length, C.byref(data), C.byref(datalen), C.byref(fin), C.byref(typ))
+    if data.value == sent:
+        return r, None, None, None, None
+    doff = None if data.value is None else data.value - base
+    return r, doff, datalen.value, fin.value, typ.value
+
+
+def websocketframeEncodeHeadLength(datalen):
+    return load_lib().websocketframeEncodeHeadLength(datalen)
+
+
+def websocketframeEncode(is_fin, prev_is_fin, type_, datalen):
+    """websocketframe.c:176-202; returns the header bytes"""
+    lib = load_lib()
+    h = (C.c_ubyte * WEBSOCKET_MAX_ENCODE_HEADLENGTH)()
+    lib.websocketframeEncode(h, is_fin, prev_is_fin, type_, datalen)
+    return bytes(h)[: lib.websocketframeEncodeHeadLength(datalen)]
+
+
+def websocketframeComputeSecAccept(sec_key):
+    lib = load_lib()
+    out = C.create_string_buffer(60)
+    r = lib.websocketframeComputeSecAccept(sec_key, len(sec_key), out)
+    return out.value.decode() if r else None
+
+
+def websocketframeDecodeHandshakeRequest(data):
+    """returns (ret, sec_key_off, sec_key_len, sec_protocol_off, sec_protocol_len); offsets
+    into ``data`` or None (NULL) / "untouched" when the C function does not write them"""
+    lib = load_lib()
+    buf = C.create_string_buffer(bytes(data), len(data))
+    sent = 0xA5A5A5A5A5A5A5A5
+    sk, skl, sp, spl = C.c_void_p(sent), C.c_uint(777), C.c_void_p(sent), C.c_uint(777)
+    r = lib.websocketframeDecodeHandshakeRequest(buf, len(data), C.byref(sk), C.byref(skl), C.byref(sp), C.byref(spl))
+    base = C.addressof(buf)
+
+    def off(p):
+        return "untouched" if p.value == sent else (None if p.value is None else p.value - base)
+    return r, off(sk), skl.value, off(sp), spl.value
+
+
+def websocketframeEncodeHandshakeResponse(sec_accept):
+    lib = load_lib()
+    out = C.create_string_buffer(162)
+    return C.string_at(lib.websocketframeEncodeHandshakeResponse(sec_accept, len(sec_accept), out)).decode()
+
+
+def websocketframeEncodeHandshakeResponseWithProtocol(sec_accept, sec_protocol):
+    lib = load_lib()
+    p = lib.websocketframeEncodeHandshakeResponseWithProtocol(
+        sec_accept, len(sec_accept), sec_protocol, len(sec_protocol) if sec_protocol else 0)
+    if not p:
+        return None
+    s = C.string_at(p).decode()
+    lib.websocketframeFreeString(p)
+    return s
+
+
+# ------------------------------------------------------------------ batch, device
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=None, stream=None):
+    """websocketframeBatchDecodeDevice on torch CUDA tensors (uint8 buf, int64 seg_off/
+    seg_len/desc_base, desc: uint8 [>= 32*slots], res: uint8 [16*nseg]); async on `stream`."""
+    nseg = seg_off.numel()
+    assert seg_len.numel() == nseg and res.numel() * res.element_size() >= 16 * nseg
+    assert buf.is_cuda and seg_off.is_cuda and seg_len.is_cuda and desc.is_cuda and res.is_cuda
+    rc = load_lib().websocketframeBatchDecodeDevice(_ptr(buf), _ptr(seg_off), _ptr(seg_len), nseg, max_frames,
+                                                    _ptr(desc_base), _ptr(desc), _ptr(res), _stream(stream))
+    check(rc, "websocketframeBatchDecodeDevice")
+
+
+def batch_decode_host(buf, seg_off, seg_len, max_frames, device=0):
+    """websocketframeBatchDecodeHost: buf (numpy uint8, modified in place), seg_off/seg_len
+    (numpy uint64). Returns (desc structured array [nseg*max_frames], res [nseg])."""
+    nseg = len(seg_off)
+    seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    seg_len = np.ascontiguousarray(seg_len, dtype=np.uint64)
+    desc = np.zeros(max(1, nseg * max_frames), dtype=DESC_DTYPE)
+    res = np.zeros(max(1, nseg), dtype=SEGRES_DTYPE)
+    rc = load_lib().websocketframeBatchDecodeHost(buf.ctypes.data, buf.nbytes, seg_off.ctypes.data,
+                                                  seg_len.ctypes.data, nseg, max_frames, desc.ctypes.data,
+                                                  res.ctypes.data, device)
+    check(rc, "websocketframeBatchDecodeHost")
+    return desc, res[:nseg]
+
+
+def synth_device(buf, frame_off, nframes, plen_kind, fixed_len, b0_kind, seed, stream=None):
+    rc = load_lib().websocketframeSynthDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, b0_kind,
+                                              seed, _stream(stream))
+    check(rc, "websocketframeSynthDevice")
+
+
+def synth_verify_device(buf, frame_off, nframes, plen_kind, fixed_len, seed, expect_plain, mismatch, stream=None):
+    rc = load_lib().websocketframeSynthVerifyDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, seed,
+                                                    1 if expect_plain else 0, _ptr(mismatch), _stream(stream))
+    check(rc, "websocketframeSynthVerifyDevice")
