@@ -220,7 +220,7 @@ def main():
     torch.cuda.synchronize()
     sample = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        sample = wl.host_sample(65536)
+        sample = wl.host_sample(262144)
 
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):

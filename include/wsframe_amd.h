@@ -102,6 +102,12 @@ typedef struct WebsocketSegResult_t {
     int status;                  /* WEBSOCKET_SEG_* */
 } WebsocketSegResult_t;
 
+/* Device batches must keep WEBSOCKET_BATCH_PAD readable bytes of device memory
+ * after the end of every segment (e.g. allocate the highest segment end + 32).
+ * The kernels may read those bytes (never write them, never use their values):
+ * it lets every header fetch be one unconditional scalar load. */
+#define WEBSOCKET_BATCH_PAD 32
+
 /* Decode a device-resident batch of rx segments in place, asynchronously on
  * `hip_stream` (hipStream_t, NULL = default stream).
  *   d_buf          batch buffer (device); payloads are unmasked in place
@@ -135,6 +141,13 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
 /* Last HIP error string of the calling thread's most recent failed call ("" if none). */
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
+/* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
+ * configuration): "dyn" (1 dynamic segment dequeue / 0 static), "unroll"
+ * (2|4|8 x 16-B chunks per lane per batch), "nt" (0 plain / 1 nontemporal
+ * loads+stores / 2 nontemporal stores), "blocks_per_cu" (0 = resident limit).
+ * Returns 0, or -1 for an unknown name. Not thread-safe against concurrent calls. */
+WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
+
 /* ---- Part 3: synthetic batches (bench / test input only, not the decode path) - */
 
 /* Fill d_buf with nframes masked frames generated by util_amd/csrc/ws_synth.h.
@@ -153,6 +166,16 @@ WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned char* d_bu
                                                        unsigned long long fixed_len, unsigned long long seed,
                                                        int expect_plain, unsigned long long* d_mismatch,
                                                        void* hip_stream);
+
+/* ---- Part 4: diagnostics (not the decode path) --------------------------------- */
+
+/* Streaming-bandwidth ceilings of this device for the decode's access pattern:
+ * flat grid-stride 16-B-per-lane kernels over nbytes (multiple of 16).
+ * mode 0: in-place XOR of d_a; 1: copy d_a -> d_b; 2: read-only d_a (d_b: 8-B sink);
+ * 3: in-place XOR software-pipelined (next loads before current stores); 4: in-place XOR one-shot blocks.
+ * nt: nontemporal loads/stores; blocks: grid size (0 = 2048). Async on hip_stream. */
+WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_b, unsigned long long nbytes, int mode, int nt,
+                                                  int blocks, void* hip_stream);
 
 #ifdef __cplusplus
 }

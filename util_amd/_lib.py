@@ -28,7 +28,7 @@ EXPORTS = [
     "websocketframeEncodeHandshakeResponse", "websocketframeEncodeHandshakeResponseWithProtocol",
     "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
     "websocketframeEncode", "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
-    "websocketframeGpuLastError", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
+    "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuCalibrate", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
 ]
 
 
@@ -71,6 +71,10 @@ def load_lib():
     lib.websocketframeBatchDecodeHost.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, i32]
     lib.websocketframeGpuLastError.restype = C.c_char_p
     lib.websocketframeGpuLastError.argtypes = []
+    lib.websocketframeGpuSetOption.restype = i32
+    lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
+    lib.websocketframeGpuCalibrate.restype = i32
+    lib.websocketframeGpuCalibrate.argtypes = [vp, vp, u64, i32, i32, i32, vp]
     lib.websocketframeSynthDevice.restype = i32
     lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
     lib.websocketframeSynthVerifyDevice.restype = i32

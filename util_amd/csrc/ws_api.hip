@@ -1,0 +1,189 @@
+// ws_api.hip — C ABI of the batch decode (include/wsframe_amd.h Part 2):
+// argument checks, per-device workspace, variant dispatch, host-buffer path.
+//
+// Default path = ws_walker.hip (one wave walks and unmasks one rx segment; fastest
+// measured so far). Variants kept for A/B measurement: "segblock" =
+// ws_segblock.hip (one workgroup per segment, one load round), "split" =
+// ws_split.hip (walk kernel + unmask kernel).
+#include <stdio.h>
+#include <string.h>
+
+#include "ws_common.h"
+
+static __thread char g_last_error[256];
+extern int ws_dbg_flags;
+
+int ws_set_err(const char* what, hipError_t e) {
+    snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
+    return -(int)(e ? e : 1);
+}
+
+int ws_set_msg(const char* msg) {
+    snprintf(g_last_error, sizeof(g_last_error), "%s", msg);
+    return -1;
+}
+
+extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { return g_last_error; }
+
+// ---------------------------------------------------------------------------------------------
+// launch configuration (tunable for in-process A/B by bench/profiling tools)
+
+struct WsTuning {
+    int path = 1;           // 0: segment blocks (ws_segblock), 1: fused walker, 2: split walk + unmask
+    int seg_cfg = 0;        // segment-block geometry: 0 256x17, 1 512x9, 2 1024x5, 3 256x8, 4 512x4
+    int split_cfg = 0;      // split unmask geometry: 0 512x9, 1 1024x5, 2 256x17, 3 512x4
+    int nt = 1;             // 0 plain, 1 nontemporal loads+stores, 2 nontemporal stores only
+    int dyn = 0;            // walker: 1 dynamic segment dequeue, 0 static grid-stride
+    int unroll = 4;         // walker: 16-B chunks per lane per batch
+    int blocks_per_cu = 64; // walker: grid cap in blocks per CU (64: one segment per wave)
+};
+static WsTuning g_tune;
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
+    if (!strcmp(name, "path")) g_tune.path = (int)value;
+    else if (!strcmp(name, "split_cfg")) g_tune.split_cfg = (int)value;
+    else if (!strcmp(name, "seg_cfg")) g_tune.seg_cfg = (int)value;
+    else if (!strcmp(name, "debug")) ws_dbg_flags = (int)value;
+    else if (!strcmp(name, "nt")) g_tune.nt = (int)value;
+    else if (!strcmp(name, "dyn")) g_tune.dyn = (int)value;
+    else if (!strcmp(name, "unroll")) g_tune.unroll = (int)value;
+    else if (!strcmp(name, "blocks_per_cu")) g_tune.blocks_per_cu = (int)value;
+    else return -1;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-device state: CU count, the walker's dequeue-counter ring, and the split
+// path's workspace (4-B key per descriptor slot + 4-B work count per segment),
+// grown on demand. Growing allocates, so size it once (a first call) before
+// capturing calls into a HIP graph. One workspace per device: concurrent calls
+// on different streams of one device must not overlap in time.
+#define WS_MAX_DEV 64
+#define WS_CTR_RING 64
+struct WsDevState {
+    int init = 0;
+    int cus = 0;
+    u32* ctr = nullptr;
+    unsigned slot = 0;
+    u32* ws = nullptr;
+    size_t ws_bytes = 0;
+};
+static WsDevState g_dev[WS_MAX_DEV];
+
+static int dev_state(WsDevState** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return ws_set_err("hipGetDevice", e);
+    if (dev < 0 || dev >= WS_MAX_DEV) return ws_set_err("device index", hipErrorInvalidDevice);
+    WsDevState& st = g_dev[dev];
+    if (!st.init) {
+        hipDeviceProp_t prop;
+        if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return ws_set_err("hipGetDeviceProperties", e);
+        st.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+        if ((e = hipMalloc(&st.ctr, WS_CTR_RING * 128)) != hipSuccess) return ws_set_err("hipMalloc(counters)", e);
+        if ((e = hipMemset(st.ctr, 0, WS_CTR_RING * 128)) != hipSuccess) return ws_set_err("hipMemset(counters)", e);
+        st.init = 1;
+    }
+    *out = &st;
+    return 0;
+}
+
+static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream) {
+    if (ds->ws_bytes >= bytes) return 0;
+    hipError_t e;
+    if (ds->ws) {
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+        (void)hipFree(ds->ws);
+        ds->ws = nullptr;
+        ds->ws_bytes = 0;
+    }
+    const size_t sz = bytes + bytes / 4 + 4096;
+    if ((e = hipMalloc(&ds->ws, sz)) != hipSuccess) return ws_set_err("hipMalloc(workspace)", e);
+    ds->ws_bytes = sz;
+    return 0;
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, const u64* d_seg_off,
+                                                                  const u64* d_seg_len, unsigned int nseg,
+                                                                  unsigned int max_frames, const u64* d_desc_base,
+                                                                  WebsocketFrameDesc_t* d_desc,
+                                                                  WebsocketSegResult_t* d_res, void* hip_stream) {
+    if (nseg == 0) return 0;
+    if (!d_buf || !d_seg_off || !d_seg_len || !d_desc || !d_res || max_frames == 0)
+        return ws_set_msg("websocketframeBatchDecodeDevice: invalid argument");
+    if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_res)) & 15)
+        return ws_set_msg("websocketframeBatchDecodeDevice: d_desc/d_res not 16-B aligned");
+    WsDevState* ds = nullptr;
+    int rc = dev_state(&ds);
+    if (rc) return rc;
+    const WsTuning t = g_tune;
+    WsLaunch L;
+    L.buf = d_buf; L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg; L.max_frames = max_frames;
+    L.desc_base = d_desc_base; L.desc = d_desc; L.res = d_res;
+    L.stream = reinterpret_cast<hipStream_t>(hip_stream);
+    L.cus = ds->cus;
+    if (t.path == 0) return ws_launch_segblock(L, t.seg_cfg, t.nt);
+    if (t.path == 1) {
+        u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
+        return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
+    }
+    const size_t nslots = (size_t)nseg * max_frames;
+    if ((rc = workspace(ds, nslots * 4 + (size_t)nseg * 4 + 256, L.stream))) return rc;
+    u32* keys = ds->ws;
+    u32* nwork = ds->ws + ((nslots + 63) & ~(size_t)63);
+    return ws_launch_split(L, t.split_cfg, t.nt, keys, nwork);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host-buffer entry point: pinned staging + H2D + kernel + D2H (synchronous)
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
+                                                                const u64* h_seg_off, const u64* h_seg_len,
+                                                                unsigned int nseg, unsigned int max_frames,
+                                                                WebsocketFrameDesc_t* h_desc,
+                                                                WebsocketSegResult_t* h_res, int device) {
+    hipError_t e;
+    unsigned char* d_buf = nullptr;
+    u64 *d_off = nullptr, *d_len = nullptr;
+    WebsocketFrameDesc_t* d_desc = nullptr;
+    WebsocketSegResult_t* d_res = nullptr;
+    hipStream_t st = nullptr;
+    int rc = 0;
+    const size_t ndesc = (size_t)nseg * max_frames;
+    if (nseg == 0) return 0;
+    if ((e = hipSetDevice(device)) != hipSuccess) return ws_set_err("hipSetDevice", e);
+#define WS_TRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = ws_set_err(what, e); goto out; } } while (0)
+    WS_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    WS_TRY(hipMalloc(&d_buf, buflen + WEBSOCKET_BATCH_PAD), "hipMalloc(buf)");
+    WS_TRY(hipMemsetAsync(d_buf + buflen, 0, WEBSOCKET_BATCH_PAD, st), "hipMemset(pad)");
+    WS_TRY(hipMalloc(&d_off, nseg * sizeof(u64)), "hipMalloc(seg_off)");
+    WS_TRY(hipMalloc(&d_len, nseg * sizeof(u64)), "hipMalloc(seg_len)");
+    WS_TRY(hipMalloc(&d_desc, (ndesc ? ndesc : 1) * sizeof(WebsocketFrameDesc_t)), "hipMalloc(desc)");
+    WS_TRY(hipMalloc(&d_res, nseg * sizeof(WebsocketSegResult_t)), "hipMalloc(res)");
+    WS_TRY(hipMemcpyAsync(d_buf, h_buf, buflen, hipMemcpyHostToDevice, st), "H2D buf");
+    WS_TRY(hipMemcpyAsync(d_off, h_seg_off, nseg * sizeof(u64), hipMemcpyHostToDevice, st), "H2D seg_off");
+    WS_TRY(hipMemcpyAsync(d_len, h_seg_len, nseg * sizeof(u64), hipMemcpyHostToDevice, st), "H2D seg_len");
+    rc = websocketframeBatchDecodeDevice(d_buf, d_off, d_len, nseg, max_frames, nullptr, d_desc, d_res, st);
+    if (rc) goto out;
+    WS_TRY(hipMemcpyAsync(h_buf, d_buf, buflen, hipMemcpyDeviceToHost, st), "D2H buf");
+    WS_TRY(hipMemcpyAsync(h_res, d_res, nseg * sizeof(WebsocketSegResult_t), hipMemcpyDeviceToHost, st), "D2H res");
+    WS_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
+    // descriptors: copy only the used prefix of every segment's slots
+    for (u32 s = 0; s < nseg; ++s) {
+        if (h_res[s].n_frames)
+            WS_TRY(hipMemcpyAsync(h_desc + (size_t)s * max_frames, d_desc + (size_t)s * max_frames,
+                                  h_res[s].n_frames * sizeof(WebsocketFrameDesc_t), hipMemcpyDeviceToHost, st),
+                   "D2H desc");
+    }
+    WS_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
+#undef WS_TRY
+out:
+    if (d_buf) (void)hipFree(d_buf);
+    if (d_off) (void)hipFree(d_off);
+    if (d_len) (void)hipFree(d_len);
+    if (d_desc) (void)hipFree(d_desc);
+    if (d_res) (void)hipFree(d_res);
+    if (st) (void)hipStreamDestroy(st);
+    return rc;
+}
+

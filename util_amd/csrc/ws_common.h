@@ -1,0 +1,211 @@
+// ws_common.h — shared device types and the RFC 6455 header parse used by every
+// decode kernel (one definition, so the walker, the split walk kernel and the
+// fallback paths cannot drift apart).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/wsframe_amd.h"
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Global-address-space views: hot loops must emit global_load/store, not flat_*
+// (flat ops complete out of order, so hipcc drains vmcnt+lgkmcnt before each one
+// and every load becomes its own round trip).
+#define WS_GLOBAL __attribute__((address_space(1)))
+typedef WS_GLOBAL u32x4 gu32x4;
+typedef WS_GLOBAL u32 gu32;
+typedef WS_GLOBAL u64 gu64;
+typedef WS_GLOBAL unsigned char gu8;
+// Constant-address-space view: wave-uniform loads through it become s_load_*.
+typedef __attribute__((address_space(4))) const u32 cu32;
+
+template <typename T>
+__device__ __forceinline__ WS_GLOBAL T* gptr(const void* p) {
+    return reinterpret_cast<WS_GLOBAL T*>(reinterpret_cast<uintptr_t>(p));
+}
+
+// Cache policy of the payload stream (A/B-able): 0 plain, 1 nontemporal loads+stores, 2 nt stores.
+template <int NT>
+__device__ __forceinline__ u32x4 ld16(const gu32x4* p) {
+    if constexpr (NT == 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st16(u32x4 v, gu32x4* p) {
+    if constexpr (NT >= 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ u32 rotl32(u32 x, u32 r) { return r ? (x << r) | (x >> (32 - r)) : x; }
+
+// Result of parsing one frame header (websocketframe.c:112-165).
+enum { WS_PARSE_INCOMPLETE = 0, WS_PARSE_FRAME = 1, WS_PARSE_WRAP = 2 };
+struct WsHdr {
+    int kind;      // WS_PARSE_*
+    u32 b0, b1;    // header bytes 0 and 1
+    u32 hdr;       // 2 + ext + mask
+    u32 masked;    // MASK bit
+    u32 key;       // little-endian masking key (valid if masked)
+    u64 plen;      // payload length
+    int ret;       // (int) return value (:164)
+};
+
+// h0 = header bytes 0..7, h1 = bytes 8..15 (little-endian), avail = bytes left (>= 2).
+// Mirrors websocketframe.c:121-164 exactly, plus the batch fence: a MASKED frame
+// whose u64 length sum wraps and would pass the :149 check is WS_PARSE_WRAP (the
+// reference would unmask past the buffer: undefined behaviour).
+__device__ __forceinline__ WsHdr ws_parse(u64 h0, u64 h1, u64 avail) {
+    WsHdr r;
+    r.b0 = (u32)h0 & 0xFFu;
+    r.b1 = (u32)(h0 >> 8) & 0xFFu;
+    const u32 p7 = r.b1 & 0x7Fu;                                   // :129
+    r.masked = r.b1 >> 7;                                          // :126-127
+    const u32 ext = p7 < 126 ? 0u : (p7 == 126 ? 2u : 8u);         // :134-145
+    r.hdr = 2u + ext + (r.masked ? 4u : 0u);
+    r.kind = WS_PARSE_INCOMPLETE;
+    r.key = 0;
+    r.plen = 0;
+    r.ret = 0;
+    if (avail < r.hdr) return r;                                   // :131,136,142
+    if (ext == 0) r.plen = p7;
+    else if (ext == 2) r.plen = ((h0 >> 16) & 0xFFu) << 8 | ((h0 >> 24) & 0xFFu);   // memReadBE16
+    else r.plen = __builtin_bswap64((h0 >> 16) | (h1 << 48));                          // memReadBE64
+    const u64 total = (u64)r.hdr + r.plen;                         // u64, may wrap (:149)
+    if (avail < total) return r;                                   // :149-150
+    if (r.masked && total < r.plen) { r.kind = WS_PARSE_WRAP; return r; }
+    r.key = ext == 0 ? (u32)(h0 >> 16) : (ext == 2 ? (u32)(h0 >> 32) : (u32)(h1 >> 16));
+    r.ret = (int)(u32)total;                                       // :164, truncating
+    r.kind = WS_PARSE_FRAME;
+    return r;
+}
+
+// Header bytes [p, p+16) from the 32 bytes x0|x1 loaded at floor16(p), o = p & 15,
+// as two little-endian u64 (bytes 0..7, 8..15). Branch-free on purpose: a divergent
+// per-lane dword select around these loads produced nondeterministic header reads
+// under load on ROCm 7.2.
+__device__ __forceinline__ void ws_hdr_from32(const u32x4 x0, const u32x4 x1, u32 o, u64& h0, u64& h1) {
+    const u64 w0 = (u64)x0.x | ((u64)x0.y << 32), w1 = (u64)x0.z | ((u64)x0.w << 32);
+    const u64 w2 = (u64)x1.x | ((u64)x1.y << 32), w3 = (u64)x1.z | ((u64)x1.w << 32);
+    const u32 sh = 8u * (o & 7);
+    const bool up = o >= 8;
+    const u64 a0 = up ? w1 : w0, a1 = up ? w2 : w1, a2 = up ? w3 : w2;
+    h0 = sh ? (a0 >> sh) | (a1 << (64 - sh)) : a0;
+    h1 = sh ? (a1 >> sh) | (a2 << (64 - sh)) : a1;
+}
+
+// Descriptor as two 16-B stores (WebsocketFrameDesc_t layout).
+__device__ __forceinline__ void ws_store_desc(WebsocketFrameDesc_t* d, u64 frame_off, const WsHdr& h) {
+    const u64 dof = h.plen ? frame_off + h.hdr : WEBSOCKET_DATA_OFF_NULL;
+    u32x4 q0, q1;
+    q0.x = (u32)frame_off; q0.y = (u32)(frame_off >> 32); q0.z = (u32)dof; q0.w = (u32)(dof >> 32);
+    q1.x = (u32)h.plen; q1.y = (u32)(h.plen >> 32); q1.z = (u32)h.ret;
+    q1.w = (h.b0 >> 7) | ((h.b0 & 0x0Fu) << 8) | (h.masked << 16) | (h.hdr << 24);
+    gu32x4* g = gptr<u32x4>(d);
+    g[0] = q0;
+    g[1] = q1;
+}
+
+__device__ __forceinline__ void ws_store_res(WebsocketSegResult_t* res, u64 consumed, u32 nf, int status) {
+    u32x4 r;
+    r.x = (u32)consumed; r.y = (u32)(consumed >> 32); r.z = nf; r.w = (u32)status;
+    *gptr<u32x4>(res) = r;
+}
+
+// Frame table entry in LDS for one round: the item's payload range relative to the
+// round start, clamped to [-16, round bytes + 16] (so 32 bits suffice for any
+// segment size), and its key pre-rotated for 16-B-aligned chunks: byte j of a
+// chunk at offset x takes key[(x + j - p0) & 3] = byte (j & 3) of rotl(key, 8*(p0 & 3)).
+// Unmasked / empty items keep their position with an empty range, so the table
+// stays sorted and non-overlapping.
+struct Item {
+    int p0, p1;
+    u32 rkey, pad;
+};
+
+__device__ __forceinline__ u32 nib_to_bytemask(u32 n) {
+    return ((n & 1u) ? 0x000000FFu : 0u) | ((n & 2u) ? 0x0000FF00u : 0u) | ((n & 4u) ? 0x00FF0000u : 0u) |
+           ((n & 8u) ? 0xFF000000u : 0u);
+}
+
+
+// One round of the unmask over chunks [0, lim] of `rb` (data already loaded into v:
+// lane `tid` holds chunk min(tid + u*T, lim) in v[u]). Wave w's slot u covers chunks
+// [u*T + 64w, +64): a wave-uniform item cursor advances monotonically over the table
+// (broadcast LDS reads) and each lane steps 0-1 items for its own chunk. Full chunks
+// take one 16-B store; chunks straddling payload edges store exactly the payload
+// bytes. Every chunk is stored by its owning lane only: clamped duplicates never store
+// (another wave may already have stored that chunk: no double XOR).
+template <int T, int U, int NT>
+__device__ __forceinline__ void ws_xor_round(const u32x4 (&v)[U], gu32x4* const rb, const u32 lim, const Item* tab,
+                                             const u32 cnt, const u32 tid) {
+    const u32 wv = tid >> 6, ln = tid & 63;
+    u32 icur = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const u32 lw = (u32)(u * T) + 64u * wv;               // wave-uniform first chunk
+        if (lw > lim) break;
+        while (icur < cnt && tab[icur].p1 <= (int)(lw * 16)) ++icur;
+        const u32 lc = lw + ln;
+        if (lc > lim) continue;   // clamped duplicate: never store (another wave may have stored it)
+        const int x = (int)(lc * 16);
+        u32 j = icur;
+        Item it = tab[j < cnt ? j : 0];
+        while (j < cnt && it.p1 <= x) { ++j; it = tab[j < cnt ? j : 0]; }
+        if (j >= cnt || it.p0 >= x + 16) continue;              // no payload byte in this chunk
+        gu32x4* const pc = rb + lc;
+        if (it.p0 <= x && it.p1 >= x + 16) {
+            st16<NT>(v[u] ^ it.rkey, pc);
+            continue;
+        }
+        // chunk straddles payload edges: OR the byte ranges of every item touching it
+        u32 m0 = 0, m1 = 0, m2 = 0, m3 = 0, cov = 0;
+        for (u32 i = j; i < cnt; ++i) {
+            const Item t = tab[i];
+            if (t.p0 >= x + 16) break;
+            const int lo = t.p0 > x ? t.p0 - x : 0, hi = t.p1 < x + 16 ? t.p1 - x : 16;
+            if (hi <= lo) continue;
+            const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+            cov |= bits;
+            m0 |= t.rkey & nib_to_bytemask(bits & 15u);
+            m1 |= t.rkey & nib_to_bytemask((bits >> 4) & 15u);
+            m2 |= t.rkey & nib_to_bytemask((bits >> 8) & 15u);
+            m3 |= t.rkey & nib_to_bytemask(bits >> 12);
+        }
+        u32x4 mm;
+        mm.x = m0; mm.y = m1; mm.z = m2; mm.w = m3;
+        const u32x4 w = v[u] ^ mm;
+        if (cov == 0xFFFFu) {
+            st16<NT>(w, pc);
+        } else {
+            gu8* const pb = reinterpret_cast<gu8*>(pc);
+#pragma unroll
+            for (u32 q = 0; q < 16; ++q) {
+                const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
+                if ((cov >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
+            }
+        }
+    }
+}
+
+// host side
+int ws_set_err(const char* what, hipError_t e);
+int ws_set_msg(const char* msg);
+
+// kernel launchers (one per translation unit)
+struct WsLaunch {
+    unsigned char* buf;
+    const u64* seg_off;
+    const u64* seg_len;
+    u32 nseg;
+    u32 max_frames;
+    const u64* desc_base;
+    WebsocketFrameDesc_t* desc;
+    WebsocketSegResult_t* res;
+    hipStream_t stream;
+    int cus;
+};
+int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr);
+int ws_launch_split(const WsLaunch& L, int variant, int nt, u32* keys, u32* nwork);
+int ws_launch_segblock(const WsLaunch& L, int cfg, int nt);

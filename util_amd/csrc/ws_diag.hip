@@ -1,0 +1,248 @@
+// ws_diag.hip — bench/test support kernels (not the decode path):
+//   * synthetic frame batches generated in HBM (ws_synth.h), and their verification;
+//   * streaming-bandwidth calibration kernels (the ceilings DESIGN.md §4 quotes).
+#include <stdio.h>
+
+#include "ws_common.h"
+#include "ws_synth.h"
+
+// ---------------------------------------------------------------------------------------------
+// synthetic batches (bench/test input; ws_synth.h)
+
+__global__ __launch_bounds__(256) void ws_synth_kernel(unsigned char* __restrict__ buf, const u64* __restrict__ frame_off,
+                                                       u64 nframes, int plen_kind, u64 fixed_len, int b0_kind,
+                                                       u64 seed) {
+    for (u64 f = blockIdx.x; f < nframes; f += gridDim.x) {
+        const u64 plen = ws_synth_plen(plen_kind, fixed_len, seed, f);
+        const u32 key = ws_synth_key(seed, f);
+        unsigned char* p = buf + frame_off[f];
+        const u32 hl = ws_synth_headlen(plen) + 4u;
+        if (threadIdx.x == 0) {
+            unsigned char h[14];
+            ws_synth_header(h, ws_synth_b0(b0_kind, f), plen, key);
+            for (u32 i = 0; i < hl; ++i) p[i] = h[i];
+        }
+        unsigned char* pl = p + hl;
+        const u64 km = (u64)key | ((u64)key << 32);
+        const u64 nw = (plen + 7) >> 3;
+        for (u64 j = threadIdx.x; j < nw; j += blockDim.x) {
+            const u64 w = ws_synth_plain_word(seed, f, j) ^ km;
+            const u64 nb = plen - 8 * j < 8 ? plen - 8 * j : 8;
+            for (u64 b = 0; b < nb; ++b) pl[8 * j + b] = (unsigned char)(w >> (8 * b));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void ws_verify_kernel(const unsigned char* __restrict__ buf,
+                                                        const u64* __restrict__ frame_off, u64 nframes, int plen_kind,
+                                                        u64 fixed_len, u64 seed, int expect_plain,
+                                                        unsigned long long* __restrict__ mismatch) {
+    u64 bad = 0;
+    for (u64 f = blockIdx.x; f < nframes; f += gridDim.x) {
+        const u64 plen = ws_synth_plen(plen_kind, fixed_len, seed, f);
+        const u32 key = ws_synth_key(seed, f);
+        const unsigned char* pl = buf + frame_off[f] + ws_synth_headlen(plen) + 4u;
+        const u64 km = expect_plain ? 0ULL : ((u64)key | ((u64)key << 32));
+        const u64 nw = (plen + 7) >> 3;
+        for (u64 j = threadIdx.x; j < nw; j += blockDim.x) {
+            const u64 w = ws_synth_plain_word(seed, f, j) ^ km;
+            const u64 nb = plen - 8 * j < 8 ? plen - 8 * j : 8;
+            for (u64 b = 0; b < nb; ++b) bad += pl[8 * j + b] != (unsigned char)(w >> (8 * b));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) bad += __shfl_down(bad, o);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(mismatch, bad);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthDevice(unsigned char* d_buf, const u64* d_frame_off,
+                                                            unsigned long long nframes, int plen_kind,
+                                                            unsigned long long fixed_len, int b0_kind,
+                                                            unsigned long long seed, void* hip_stream) {
+    if (!nframes) return 0;
+    const u32 blocks = nframes < 65536 ? (u32)nframes : 65536u;
+    hipLaunchKernelGGL(ws_synth_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
+                       d_frame_off, (u64)nframes, plen_kind, (u64)fixed_len, b0_kind, (u64)seed);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ws_set_err("ws_synth_kernel launch", e);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned char* d_buf, const u64* d_frame_off,
+                                                                  unsigned long long nframes, int plen_kind,
+                                                                  unsigned long long fixed_len,
+                                                                  unsigned long long seed, int expect_plain,
+                                                                  unsigned long long* d_mismatch, void* hip_stream) {
+    if (!nframes) return 0;
+    const u32 blocks = nframes < 65536 ? (u32)nframes : 65536u;
+    hipLaunchKernelGGL(ws_verify_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
+                       d_frame_off, (u64)nframes, plen_kind, (u64)fixed_len, (u64)seed, expect_plain, d_mismatch);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ws_set_err("ws_verify_kernel launch", e);
+}
+
+// ---------------------------------------------------------------------------------------------
+// diagnostics: streaming ceilings on this device for the decode's access pattern
+// (flat grid-stride, 16 B per lane, no frame structure). mode 0: in-place XOR
+// (read+write the same bytes, like the unmask); mode 1: copy src -> dst; mode 2: read-only.
+
+template <int NT, int MODE>
+__global__ __launch_bounds__(256) void ws_calib_kernel(gu32x4* __restrict__ a, gu32x4* __restrict__ b, u64 n,
+                                                       u32 key, unsigned long long* __restrict__ sink) {
+    const u64 stride = (u64)gridDim.x * 256 * 4;
+    u32 acc = 0;
+    for (u64 i = (u64)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const u64 j = i + 256u * u;
+            v[u] = j < n ? ld16<NT>(a + j) : (u32x4)0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const u64 j = i + 256u * u;
+            if (MODE == 0 && j < n) st16<NT>(v[u] ^ key, a + j);
+            if (MODE == 1 && j < n) st16<NT>(v[u], b + j);
+            if (MODE == 2) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+    }
+    if (MODE == 2 && acc == 0x9E3779B9u) atomicAdd(sink, 1ull);
+}
+
+// mode 3: in-place XOR, software-pipelined: the next iteration's loads issue
+// BEFORE this iteration's stores, so waiting for loads never waits for stores.
+template <int NT>
+__global__ __launch_bounds__(256) void ws_calib_pipe_kernel(gu32x4* __restrict__ a, u64 n, u32 key) {
+    // branch-free body (clamped indices, benign duplicate stores of identical values) so
+    // the waitcnt pass sees one path: wait for `cur` = vmcnt(4) with `nxt` still in flight
+    const u64 stride = (u64)gridDim.x * 1024;
+    u64 i = (u64)blockIdx.x * 1024 + threadIdx.x;
+    const u64 last = n - 1;
+    const u32 iters = (u32)((n + stride - 1) / stride);
+    u32x4 cur[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = ld16<NT>(a + min(i + 256u * u, last));
+    for (u32 it = 0; it < iters; ++it) {
+        const u64 nx = i + stride;
+        u32x4 nxt[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) nxt[u] = ld16<NT>(a + min(nx + 256u * u, last));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) st16<NT>(cur[u] ^ key, a + min(i + 256u * u, last));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+        i = nx;
+    }
+}
+
+// mode 4: in-place XOR, one-shot blocks (no loop; 16 KiB per 256-thread block)
+template <int NT>
+__global__ __launch_bounds__(256) void ws_calib_oneshot_kernel(gu32x4* __restrict__ a, u64 n, u32 key) {
+    const u64 i = (u64)blockIdx.x * 1024 + threadIdx.x;
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld16<NT>(a + min(i + 256u * u, n - 1));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i + 256u * u < n) st16<NT>(v[u] ^ key, a + i + 256u * u);
+}
+
+// mode 5+K: in-place XOR, one-shot blocks that each do K rounds of (4 loads, 4 stores)
+template <int NT, int K>
+__global__ __launch_bounds__(256) void ws_calib_rounds_kernel(gu32x4* __restrict__ a, u64 n, u32 key) {
+    const u64 last = n - 1;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+        const u64 i = ((u64)blockIdx.x * K + k) * 1024 + threadIdx.x;
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld16<NT>(a + min(i + 256u * u, last));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) st16<NT>(v[u] ^ key, a + min(i + 256u * u, last));
+    }
+}
+
+// mode 16+: one-shot in-place XOR through buffer instructions with explicit cache
+// bits (aux: bit0 sc0, bit1 nt, bit4 sc1), T threads x U chunks per block.
+template <int T, int U, int LAUX, int SAUX>
+__global__ __launch_bounds__(T) void ws_calib_buf_kernel(unsigned char* __restrict__ a, u64 nbytes, u32 key) {
+    const u64 blk = (u64)blockIdx.x * (T * U * 16);
+    const u64 left = nbytes - blk;
+    const u32 nrec = left < (u64)(T * U * 16) ? (u32)left : (u32)(T * U * 16);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a + blk, (short)0, (int)nrec, 0x00020000);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (threadIdx.x + u * T) * 16, 0, LAUX));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v[u] ^ key), rs,
+                                               (threadIdx.x + u * T) * 16, 0, SAUX);
+}
+
+template <int T, int U, int LAUX, int SAUX>
+static void cal_buf(unsigned char* a, u64 n, hipStream_t st) {
+    const u64 per = (u64)T * U * 16;
+    hipLaunchKernelGGL((ws_calib_buf_kernel<T, U, LAUX, SAUX>), dim3((u32)((n + per - 1) / per)), dim3(T), 0, st, a, n,
+                       0x5A5A5A5Au);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_b, unsigned long long nbytes, int mode,
+                                                             int nt, int blocks, void* hip_stream) {
+    const u64 n = nbytes / 16;
+    if (blocks <= 0) blocks = 2048;
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    gu32x4* a = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_a));
+    gu32x4* b = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(d_b));
+    unsigned long long* sink = reinterpret_cast<unsigned long long*>(d_b);
+    if (mode == 3) {
+        if (nt) hipLaunchKernelGGL((ws_calib_pipe_kernel<1>), dim3(blocks), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL((ws_calib_pipe_kernel<0>), dim3(blocks), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_pipe_kernel launch", e);
+    }
+    if (mode == 4) {
+        const u64 nb = (n + 1023) / 1024;
+        if (nt) hipLaunchKernelGGL((ws_calib_oneshot_kernel<1>), dim3((u32)nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL((ws_calib_oneshot_kernel<0>), dim3((u32)nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_oneshot_kernel launch", e);
+    }
+    if (mode >= 16) {
+        unsigned char* a8 = reinterpret_cast<unsigned char*>(d_a);
+        const u64 nb = n * 16;
+        switch (mode) {
+        case 16: cal_buf<256, 4, 2, 2>(a8, nb, st); break;
+        case 17: cal_buf<256, 4, 0, 0>(a8, nb, st); break;
+        case 18: cal_buf<256, 4, 2, 16>(a8, nb, st); break;
+        case 19: cal_buf<256, 4, 2, 0>(a8, nb, st); break;
+        case 20: cal_buf<256, 4, 0, 2>(a8, nb, st); break;
+        case 21: cal_buf<256, 8, 2, 2>(a8, nb, st); break;
+        case 22: cal_buf<512, 4, 2, 2>(a8, nb, st); break;
+        case 23: cal_buf<1024, 4, 2, 2>(a8, nb, st); break;
+        case 24: cal_buf<256, 2, 2, 2>(a8, nb, st); break;
+        case 25: cal_buf<256, 16, 2, 2>(a8, nb, st); break;
+        case 26: cal_buf<256, 4, 3, 3>(a8, nb, st); break;
+        case 27: cal_buf<256, 4, 2, 18>(a8, nb, st); break;
+        case 28: cal_buf<128, 4, 2, 2>(a8, nb, st); break;
+        case 29: cal_buf<64, 4, 2, 2>(a8, nb, st); break;
+        default: return ws_set_msg("websocketframeGpuCalibrate: unknown mode");
+        }
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_buf_kernel launch", e);
+    }
+    if (mode >= 5 && mode <= 8) {
+        const int K = mode == 5 ? 1 : (mode == 6 ? 2 : (mode == 7 ? 4 : 16));
+        const u32 nb = (u32)((n + 1024ull * K - 1) / (1024ull * K));
+        if (K == 1) hipLaunchKernelGGL((ws_calib_rounds_kernel<1, 1>), dim3(nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        if (K == 2) hipLaunchKernelGGL((ws_calib_rounds_kernel<1, 2>), dim3(nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        if (K == 4) hipLaunchKernelGGL((ws_calib_rounds_kernel<1, 4>), dim3(nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        if (K == 16) hipLaunchKernelGGL((ws_calib_rounds_kernel<1, 16>), dim3(nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_rounds_kernel launch", e);
+    }
+#define WS_CAL(NTV, M) hipLaunchKernelGGL((ws_calib_kernel<NTV, M>), dim3(blocks), dim3(256), 0, st, a, b, n, 0x5A5A5A5Au, sink)
+    if (nt) { if (mode == 0) WS_CAL(1, 0); else if (mode == 1) WS_CAL(1, 1); else WS_CAL(1, 2); }
+    else { if (mode == 0) WS_CAL(0, 0); else if (mode == 1) WS_CAL(0, 1); else WS_CAL(0, 2); }
+#undef WS_CAL
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ws_set_err("ws_calib_kernel launch", e);
+}

@@ -22,6 +22,7 @@ WEBSOCKET_MAX_ENCODE_HEADLENGTH = 10
 
 SEG_OK, SEG_MAX_FRAMES, SEG_ERR_DECODE, SEG_ERR_LEN_WRAP = 0, 1, -1, -2
 DATA_OFF_NULL = 0xFFFFFFFFFFFFFFFF
+BATCH_PAD = 32  # WEBSOCKET_BATCH_PAD: readable device bytes required after every segment
 
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("data_off", "<u8"), ("datalen", "<u8"), ("ret", "<i4"),
                        ("is_fin", "u1"), ("type", "u1"), ("masked", "u1"), ("hdrlen", "u1")])
@@ -127,6 +128,7 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
     """websocketframeBatchDecodeDevice on torch CUDA tensors (uint8 buf, int64 seg_off/
     seg_len/desc_base, desc: uint8 [>= 32*slots], res: uint8 [16*nseg]); async on `stream`."""
     nseg = seg_off.numel()
+    assert buf.numel() >= BATCH_PAD, "device batch needs WEBSOCKET_BATCH_PAD bytes of slack"
     assert seg_len.numel() == nseg and res.numel() * res.element_size() >= 16 * nseg
     assert buf.is_cuda and seg_off.is_cuda and seg_len.is_cuda and desc.is_cuda and res.is_cuda
     rc = load_lib().websocketframeBatchDecodeDevice(_ptr(buf), _ptr(seg_off), _ptr(seg_len), nseg, max_frames,
@@ -159,3 +161,10 @@ def synth_verify_device(buf, frame_off, nframes, plen_kind, fixed_len, seed, exp
     rc = load_lib().websocketframeSynthVerifyDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, seed,
                                                     1 if expect_plain else 0, _ptr(mismatch), _stream(stream))
     check(rc, "websocketframeSynthVerifyDevice")
+
+
+def set_option(name, value):
+    """websocketframeGpuSetOption (launch tuning knobs, for A/B measurement)"""
+    rc = load_lib().websocketframeGpuSetOption(name.encode(), int(value))
+    if rc != 0:
+        raise ValueError("unknown option %r" % name)
