@@ -24,6 +24,26 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+# kernel that dominates the step, per websocketframeGpuSetOption("path") value
+KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel"}
+DEFAULT_PATH = 1
+
+
+def pmc_traffic(kernel, algo_bytes):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this kernel
+    and workload (profiles/<tag>_pmc.json, tools/prof_summary.py), else None."""
+    import glob
+    best = None
+    for f in glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")):
+        try:
+            rec = json.load(open(f))
+        except ValueError:
+            continue
+        if kernel in rec.get("kernel", "") and rec.get("algo_bytes_per_launch") == algo_bytes \
+                and rec.get("traffic_bytes_per_launch"):
+            if best is None or os.path.getmtime(f) > os.path.getmtime(best[0]):
+                best = (f, rec)
+    return best
 
 
 class Workload:
@@ -203,7 +223,12 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     args = ap.parse_args()
+    from util_amd import wsframe as W
+    path = DEFAULT_PATH if args.path is None else args.path
+    if args.path is not None:
+        W.set_option("path", args.path)
 
     import torch
     import torch.distributed as dist
@@ -257,6 +282,7 @@ def main():
     value = payload_all / elapsed / 2**30
     mean_kern = float(kern_ms.mean()) / 1e3
     achieved = wl.algo_bytes / mean_kern / 1e9
+    pmc = pmc_traffic(KERNELS[path], wl.algo_bytes)
     out = {
         "metric": "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames",
         "value": round(value, 2),
@@ -275,8 +301,10 @@ def main():
                    "wire_bytes_per_gpu": wl.wire_bytes, "payload_bytes_per_gpu": wl.payload_bytes,
                    "parallelism": "frame-range shards, %d independent GPU(s)" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "kernel": "ws_decode_segments_kernel", "algo_bytes_per_launch": wl.algo_bytes,
+                     "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
+                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
+                     "kernel": KERNELS[path], "algo_bytes_per_launch": wl.algo_bytes,
                      "kernel_ms_mean": round(mean_kern * 1e3, 4), "kernel_ms_min": round(float(kern_ms.min()), 4)},
         "verified": mism == 0,
         "cpu_baseline": None,

@@ -1,0 +1,65 @@
+"""Summarise a rocprofv3 run of bench.py into profiles/ (committed evidence).
+
+    python tools/prof_summary.py gpurun_out/r01 r01 [--kernel ws_walker_kernel]
+
+Inputs (written by tools/profile.sh on the GPU box):
+  <dir>/trace/run_kernel_stats.csv       rocprofv3 --kernel-trace --stats
+  <dir>/pmc_fetch/run_counter_collection.csv   rocprofv3 --pmc FETCH_SIZE
+  <dir>/pmc_write/run_counter_collection.csv   rocprofv3 --pmc WRITE_SIZE
+  <dir>/bench.json                        the bench line of the same code
+Outputs: profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_pmc.json,
+profiles/<tag>_bench.json.
+
+HBM traffic per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are
+in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
+streaming read, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, kernel, counter):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    kernel = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "ws_walker_kernel"
+    out = os.path.join(REPO, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, tag + "_kernel_stats.csv"))
+    stats = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))) if kernel in r["Name"]]
+    fetch_kib, nf = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kernel, "FETCH_SIZE")
+    write_kib, nw = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kernel, "WRITE_SIZE")
+    bench = json.load(open(os.path.join(src, "bench.json")))
+    algo = bench["roofline"]["algo_bytes_per_launch"]
+    rec = {
+        "kernel": stats[0]["Name"] if stats else kernel,
+        "rocprof_calls": int(stats[0]["Calls"]) if stats else 0,
+        "rocprof_avg_ns": float(stats[0]["AverageNs"]) if stats else None,
+        "rocprof_min_ns": float(stats[0]["MinNs"]) if stats else None,
+        "bench_kernel_ms_mean": bench["roofline"]["kernel_ms_mean"],
+        "fetch_size_kib_per_launch": fetch_kib, "fetch_dispatches": nf,
+        "write_size_kib_per_launch": write_kib, "write_dispatches": nw,
+        "fetch_bytes_corrected": 2 * fetch_kib * 1024 if fetch_kib is not None else None,
+        "write_bytes": write_kib * 1024 if write_kib is not None else None,
+        "algo_bytes_per_launch": algo,
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB -> bytes",
+    }
+    if fetch_kib is not None and write_kib is not None:
+        rec["traffic_bytes_per_launch"] = (2 * fetch_kib + write_kib) * 1024
+        rec["traffic_over_algo"] = rec["traffic_bytes_per_launch"] / algo
+    json.dump(rec, open(os.path.join(out, tag + "_pmc.json"), "w"), indent=1)
+    json.dump(bench, open(os.path.join(out, tag + "_bench.json"), "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
