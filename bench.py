@@ -266,17 +266,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    from util_amd import dist as D
+    elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
 
     # correctness of the timed run: after an odd number of decodes the buffer holds plaintext
     mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
-    if world > 1:
-        mt = torch.tensor([mism], dtype=torch.int64, device=dev)
-        dist.all_reduce(mt)
-        mism = int(mt.item())
+    mism = int(D.allreduce([mism], device=dev)[0])
 
     payload_all = wl.payload_bytes * world * args.steps
     value = payload_all / elapsed / 2**30
