@@ -79,6 +79,11 @@ def load_lib():
     lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
     lib.websocketframeSynthVerifyDevice.restype = i32
     lib.websocketframeSynthVerifyDevice.argtypes = [vp, vp, u64, i32, u64, u64, i32, vp, vp]
+    # launch tuning from the environment, e.g. WSFRAME_AMD_OPTIONS="path=0,seg_cfg=10"
+    for kv in filter(None, os.environ.get("WSFRAME_AMD_OPTIONS", "").split(",")):
+        name, _, value = kv.partition("=")
+        if lib.websocketframeGpuSetOption(name.strip().encode(), int(value)) != 0:
+            raise ValueError("WSFRAME_AMD_OPTIONS: unknown option %r" % name)
     _lib = lib
     return lib
 

@@ -130,6 +130,40 @@ __device__ __forceinline__ u32 nib_to_bytemask(u32 n) {
 }
 
 
+// Chunk at round offset x straddles payload edges: OR the byte ranges of every
+// table item from j on that touches it, XOR, and store exactly those bytes (one
+// 16-B store if the chunk turns out fully covered).
+template <int NT>
+__device__ __forceinline__ void ws_store_partial(const u32x4 v, gu32x4* const pc, const Item* tab, u32 j,
+                                                 const u32 cnt, const int x) {
+    u32 m0 = 0, m1 = 0, m2 = 0, m3 = 0, cov = 0;
+    for (u32 i = j; i < cnt; ++i) {
+        const Item t = tab[i];
+        if (t.p0 >= x + 16) break;
+        const int lo = t.p0 > x ? t.p0 - x : 0, hi = t.p1 < x + 16 ? t.p1 - x : 16;
+        if (hi <= lo) continue;
+        const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+        cov |= bits;
+        m0 |= t.rkey & nib_to_bytemask(bits & 15u);
+        m1 |= t.rkey & nib_to_bytemask((bits >> 4) & 15u);
+        m2 |= t.rkey & nib_to_bytemask((bits >> 8) & 15u);
+        m3 |= t.rkey & nib_to_bytemask(bits >> 12);
+    }
+    u32x4 mm;
+    mm.x = m0; mm.y = m1; mm.z = m2; mm.w = m3;
+    const u32x4 w = v ^ mm;
+    if (cov == 0xFFFFu) {
+        st16<NT>(w, pc);
+    } else if (cov) {
+        gu8* const pb = reinterpret_cast<gu8*>(pc);
+#pragma unroll
+        for (u32 q = 0; q < 16; ++q) {
+            const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
+            if ((cov >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
+        }
+    }
+}
+
 // One round of the unmask over chunks [0, lim] of `rb` (data already loaded into v:
 // lane `tid` holds chunk min(tid + u*T, lim) in v[u]). Wave w's slot u covers chunks
 // [u*T + 64w, +64): a wave-uniform item cursor advances monotonically over the table
@@ -159,33 +193,7 @@ __device__ __forceinline__ void ws_xor_round(const u32x4 (&v)[U], gu32x4* const 
             st16<NT>(v[u] ^ it.rkey, pc);
             continue;
         }
-        // chunk straddles payload edges: OR the byte ranges of every item touching it
-        u32 m0 = 0, m1 = 0, m2 = 0, m3 = 0, cov = 0;
-        for (u32 i = j; i < cnt; ++i) {
-            const Item t = tab[i];
-            if (t.p0 >= x + 16) break;
-            const int lo = t.p0 > x ? t.p0 - x : 0, hi = t.p1 < x + 16 ? t.p1 - x : 16;
-            if (hi <= lo) continue;
-            const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
-            cov |= bits;
-            m0 |= t.rkey & nib_to_bytemask(bits & 15u);
-            m1 |= t.rkey & nib_to_bytemask((bits >> 4) & 15u);
-            m2 |= t.rkey & nib_to_bytemask((bits >> 8) & 15u);
-            m3 |= t.rkey & nib_to_bytemask(bits >> 12);
-        }
-        u32x4 mm;
-        mm.x = m0; mm.y = m1; mm.z = m2; mm.w = m3;
-        const u32x4 w = v[u] ^ mm;
-        if (cov == 0xFFFFu) {
-            st16<NT>(w, pc);
-        } else {
-            gu8* const pb = reinterpret_cast<gu8*>(pc);
-#pragma unroll
-            for (u32 q = 0; q < 16; ++q) {
-                const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
-                if ((cov >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
-            }
-        }
+        ws_store_partial<NT>(v[u], pc, tab, j, cnt, x);
     }
 }
 
