@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=4303355904)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--modes", default="")
+    ap.add_argument("--modes", default="", help="comma list of mode[:blocks]")
     args = ap.parse_args()
     import torch
     from util_amd import load_lib
@@ -29,24 +29,30 @@ def main():
         names = {16: "buf256x4_nt_nt", 17: "buf256x4_plain", 18: "buf256x4_nt_sc1", 19: "buf256x4_nt_plain",
                  20: "buf256x4_plain_nt", 21: "buf256x8_nt", 22: "buf512x4_nt", 23: "buf1024x4_nt",
                  24: "buf256x2_nt", 25: "buf256x16_nt", 26: "buf256x4_sc0nt", 27: "buf256x4_nt_sc1nt",
-                 28: "buf128x4_nt", 29: "buf64x4_nt", 5: "rounds1"}
+                 28: "buf128x4_nt", 29: "buf64x4_nt", 5: "rounds1", 4: "oneshot",
+                 40: "ldspipe512x6_c3", 41: "ldspipe512x8_c3", 42: "ldspipe256x12_c3", 43: "ldspipe1024x3_c3",
+                 44: "ldspipe512x6_c1", 45: "ldspipe512x6_c7", 46: "ldspipe256x8_c3", 47: "ldspipe512x6_il",
+                 48: "ldspipe256x8_il", 49: "ldspipe1024x3_il"}
         res = {}
         for r in range(3):
-            for mode in [int(m) for m in args.modes.split(",")]:
+            for spec in args.modes.split(","):
+                mode, _, blocks = spec.partition(":")
+                mode, blocks = int(mode), int(blocks or 0)
                 ts = []
                 for i in range(args.iters + 1):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    rc = lib.websocketframeGpuCalibrate(a.data_ptr(), b.data_ptr(), n, mode, 1, 0, st)
+                    rc = lib.websocketframeGpuCalibrate(a.data_ptr(), b.data_ptr(), n, mode, 1, blocks, st)
                     e1.record()
                     assert rc == 0, lib.websocketframeGpuLastError()
                     torch.cuda.synchronize()
                     if i:
                         ts.append(e0.elapsed_time(e1))
-                res.setdefault(mode, []).extend(ts)
-        for mode, ts in res.items():
+                res.setdefault(spec, []).extend(ts)
+        for spec, ts in res.items():
             med = float(np.median(ts))
-            print(json.dumps({"kernel": names.get(mode, mode), "mode": mode, "median_ms": round(med, 4),
+            mode = int(spec.partition(":")[0])
+            print(json.dumps({"kernel": names.get(mode, mode), "mode": spec, "median_ms": round(med, 4),
                               "GBps": round(2 * n / med / 1e6, 1)}), flush=True)
         return
     for mode, name, traffic in ((0, "inplace_xor", 2 * n), (3, "inplace_xor_pipelined", 2 * n),

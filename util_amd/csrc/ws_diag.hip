@@ -178,6 +178,63 @@ __global__ __launch_bounds__(T) void ws_calib_buf_kernel(unsigned char* __restri
                                                (threadIdx.x + u * T) * 16, 0, SAUX);
 }
 
+// mode 40+: in-place XOR through an LDS pipeline. Wave 0 only issues LDS-DMA loads
+// (global_load_lds, D stages of S chunks in flight, never a store, never an LDS read,
+// so its vmcnt waits cover only its own loads); waves 1..NC only read LDS and store
+// (never a global load, so no store ever delays a load). One barrier per stage.
+typedef __attribute__((address_space(3))) void ws_lds_void;
+template <int S, int D, int NC, bool IL>
+__global__ __launch_bounds__(64 * (NC + 1)) void ws_calib_ldspipe_kernel(gu32x4* __restrict__ a, u64 nstages,
+                                                                        u32 key) {
+    constexpr int R = D + 1, NI = S / 64;
+    static_assert(S % 64 == 0 && (D - 1) * NI <= 63, "vmcnt immediate");
+    __shared__ __attribute__((aligned(16))) u32x4 lbuf[R * S];
+    const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // IL: block b takes stages b, b+G, ... (all blocks stream one compact window);
+    // otherwise one contiguous range per block
+    const u64 per = (nstages + gridDim.x - 1) / gridDim.x;
+    const u64 q0 = IL ? 0 : (u64)blockIdx.x * per;
+    const u64 q1 = IL ? 0 : (q0 + per < nstages ? q0 + per : nstages);
+    const u64 Q = IL ? (blockIdx.x < nstages ? (nstages - 1 - blockIdx.x) / gridDim.x + 1 : 0) : (q1 > q0 ? q1 - q0 : 0);
+    if (Q == 0) return;
+    auto stage = [&](u64 t) -> u64 { return IL ? t * gridDim.x + blockIdx.x : q0 + t; };
+    auto issue = [&](u64 t) {
+        gu32x4* g = a + stage(t) * S;
+        u32x4* l = &lbuf[(t % R) * S];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const WS_GLOBAL void*>(g + i * 64 + lane),
+                                             (ws_lds_void*)(l + i * 64), 16, 0, 2);
+    };
+    if (wv == 0) {
+        for (u64 t = 0; t < (u64)D && t < Q; ++t) issue(t);
+        if (Q >= (u64)D) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (u64 t = 0; t < Q; ++t) {
+        if (wv == 0) {
+            if (t + D < Q) {
+                issue(t + D);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * NI) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        } else {
+            const u32x4* l = &lbuf[(t % R) * S];
+            gu32x4* g = a + stage(t) * S;
+            for (u32 c = (wv - 1) * 64 + lane; c < (u32)S; c += NC * 64) st16<1>(l[c] ^ key, g + c);
+        }
+        __syncthreads();
+    }
+}
+
+template <int S, int D, int NC, bool IL = false>
+static void cal_ldspipe(gu32x4* a, u64 n, int blocks, hipStream_t st) {
+    hipLaunchKernelGGL((ws_calib_ldspipe_kernel<S, D, NC, IL>), dim3(blocks), dim3(64 * (NC + 1)), 0, st, a, n / S,
+                       0x5A5A5A5Au);
+}
+
 template <int T, int U, int LAUX, int SAUX>
 static void cal_buf(unsigned char* a, u64 n, hipStream_t st) {
     const u64 per = (u64)T * U * 16;
@@ -205,6 +262,23 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         else hipLaunchKernelGGL((ws_calib_oneshot_kernel<0>), dim3((u32)nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_oneshot_kernel launch", e);
+    }
+    if (mode >= 40) {  // LDS pipeline; n must be a multiple of the stage size (1024 chunks covers all)
+        switch (mode) {
+        case 40: cal_ldspipe<512, 6, 3>(a, n, blocks, st); break;
+        case 41: cal_ldspipe<512, 8, 3>(a, n, blocks, st); break;
+        case 42: cal_ldspipe<256, 12, 3>(a, n, blocks, st); break;
+        case 43: cal_ldspipe<1024, 3, 3>(a, n, blocks, st); break;
+        case 44: cal_ldspipe<512, 6, 1>(a, n, blocks, st); break;
+        case 45: cal_ldspipe<512, 6, 7>(a, n, blocks, st); break;
+        case 46: cal_ldspipe<256, 8, 3>(a, n, blocks, st); break;
+        case 47: cal_ldspipe<512, 6, 3, true>(a, n, blocks, st); break;
+        case 48: cal_ldspipe<256, 8, 3, true>(a, n, blocks, st); break;
+        case 49: cal_ldspipe<1024, 3, 3, true>(a, n, blocks, st); break;
+        default: return ws_set_msg("websocketframeGpuCalibrate: unknown mode");
+        }
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_ldspipe_kernel launch", e);
     }
     if (mode >= 16) {
         unsigned char* a8 = reinterpret_cast<unsigned char*>(d_a);
