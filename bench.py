@@ -157,6 +157,38 @@ class Workload:
         self.torch.cuda.empty_cache()
 
 
+def end_to_end(wl, runs=2):
+    """websocketframeBatchDecodeHost on a pinned host copy of the whole batch: H2D + decode + D2H,
+    pipelined over ~64 MiB segment groups on 3 streams (SURVEY §8d end-to-end). Reported beside
+    `value`, never as it. Leaves wl.buf decoded an odd number of extra times (returned in `flips`)."""
+    import torch
+    from util_amd.wsframe import DESC_DTYPE, SEGRES_DTYPE
+    from util_amd import load_lib
+    hb = torch.empty(wl.wire_bytes, dtype=torch.uint8, pin_memory=True)
+    hb.copy_(wl.buf[:wl.wire_bytes])
+    desc = torch.empty(wl.nseg * wl.fps * 32, dtype=torch.uint8, pin_memory=True)
+    res = torch.empty(wl.nseg * 16, dtype=torch.uint8, pin_memory=True)
+    so = np.ascontiguousarray(wl.seg_off_h, dtype=np.uint64)
+    sl = np.ascontiguousarray(wl.seg_len_h, dtype=np.uint64)
+    lib = load_lib()
+
+    def once():
+        rc = lib.websocketframeBatchDecodeHost(hb.data_ptr(), wl.wire_bytes, so.ctypes.data, sl.ctypes.data, wl.nseg,
+                                               wl.fps, desc.data_ptr(), res.data_ptr(), torch.cuda.current_device())
+        if rc:
+            raise RuntimeError(lib.websocketframeGpuLastError().decode())
+    torch.cuda.synchronize()
+    once()                                             # warm: slot allocation
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        once()
+    dt = (time.perf_counter() - t0) / runs
+    wl.buf[:wl.wire_bytes].copy_(hb, non_blocking=False)
+    return {"value": round(wl.payload_bytes / dt / 2**30, 2), "unit": "GiB/s", "ms": round(dt * 1e3, 2),
+            "runs": runs, "host_buffer": "pinned (hipHostMalloc via torch pin_memory)",
+            "path": "websocketframeBatchDecodeHost: H2D | decode | D2H over 64 MiB groups, 3 streams"}, runs + 1
+
+
 def cpu_baseline(sample, threads, min_seconds=1.0):
     """time the reference's own websocketframeDecode (oracle/_ref, reactor loop driver) —
     or the oracle restatement when the reference build is absent — on host cores"""
@@ -224,6 +256,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     args = ap.parse_args()
     from util_amd import wsframe as W
     path = DEFAULT_PATH if args.path is None else args.path
@@ -271,6 +304,13 @@ def main():
 
     # correctness of the timed run: after an odd number of decodes the buffer holds plaintext
     mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e, flips = end_to_end(wl)
+        wl.decodes += flips
+        e2e_mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
+        e2e["verified"] = e2e_mism == 0
+        mism += e2e_mism
     mism = int(D.allreduce([mism], device=dev)[0])
 
     payload_all = wl.payload_bytes * world * args.steps
@@ -303,6 +343,7 @@ def main():
                      "kernel_ms_mean": round(mean_kern * 1e3, 4), "kernel_ms_min": round(float(kern_ms.min()), 4)},
         "verified": mism == 0,
         "cpu_baseline": None,
+        "e2e": e2e,
     }
     if sample is not None:
         out["cpu_baseline"] = cpu_baseline(sample, min(args.cpu_threads, os.cpu_count() or 1))

@@ -129,9 +129,14 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, con
                                                        WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
                                                        void* hip_stream);
 
-/* Same, but buffers live in host memory (the reactor's m_inbuf): pinned
- * staging, H2D, kernel, D2H, synchronous. Segment offsets are relative to h_buf.
- * h_desc must hold nseg*max_frames descriptors (desc_base form not offered). */
+/* Same, but buffers live in host memory (the reactor's m_inbuf), synchronous.
+ * Segment offsets are relative to h_buf. Pipelined: groups of consecutive
+ * ascending segments (~64 MiB, option "host_chunk_mb") are copied H2D, decoded
+ * and copied back D2H on three streams, so both copy directions and the kernel
+ * overlap; any other segment layout is one group. Pass pinned memory
+ * (hipHostMalloc / hipHostRegister) for asynchronous DMA; pageable memory works
+ * through the runtime's staging copies. h_desc must hold nseg*max_frames
+ * descriptors (desc_base form not offered); slots past n_frames are zeroed. */
 WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
                                                      const unsigned long long* h_seg_off,
                                                      const unsigned long long* h_seg_len, unsigned int nseg,
@@ -142,7 +147,7 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
- * configuration): "dyn" (1 dynamic segment dequeue / 0 static), "unroll"
+ * configuration): "path" (0 segment blocks, 1 walker, 2 split), "host_chunk_mb", "dyn" (1 dynamic segment dequeue / 0 static), "unroll"
  * (2|4|8 x 16-B chunks per lane per batch), "nt" (0 plain / 1 nontemporal
  * loads+stores / 2 nontemporal stores), "blocks_per_cu" (0 = resident limit).
  * Returns 0, or -1 for an unknown name. Not thread-safe against concurrent calls. */

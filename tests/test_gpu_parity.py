@@ -220,3 +220,42 @@ def test_full_size_properties(dev, cfg):
         assert wl.verify(expect_plain=False) == 0
     finally:
         wl.free()
+
+
+def _host_vs_oracle(wire, so, sl, max_frames, tag):
+    hb = wire.copy()
+    gd, gr = W.batch_decode_host(hb, np.asarray(so, np.uint64), np.asarray(sl, np.uint64), max_frames)
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, so, sl, max_frames)
+    assert np.array_equal(gr, orr), tag
+    assert np.array_equal(used_descs(gd, gr, max_frames), used_descs(od, orr, max_frames)), tag
+    assert np.array_equal(hb, ob), tag
+    # slots past n_frames come back zeroed
+    for s in range(len(so)):
+        assert not gd[s * max_frames + int(gr[s]["n_frames"]):(s + 1) * max_frames].view(np.uint8).any(), tag
+
+
+@pytest.mark.parametrize("chunk_mb", [64, 1])
+def test_host_path_pipelined(dev, chunk_mb):
+    """websocketframeBatchDecodeHost: ascending segments split into many ~1 MiB groups
+    (3-stream H2D / decode / D2H pipeline) and the single-group case, vs the oracle"""
+    rng = np.random.default_rng(11)
+    wire, so, sl = random_stream(rng, 3000, max_frame=20000)
+    W.set_option("host_chunk_mb", chunk_mb)
+    try:
+        _host_vs_oracle(wire, so, sl, 16, "chunk %d MiB" % chunk_mb)
+    finally:
+        W.set_option("host_chunk_mb", 64)
+
+
+def test_host_path_unordered_segments(dev):
+    """segments out of buffer order: decoded as one group spanning all of them"""
+    rng = np.random.default_rng(12)
+    wire, so, sl = random_stream(rng, 800)
+    perm = rng.permutation(len(so))
+    so2, sl2 = [so[i] for i in perm], [sl[i] for i in perm]
+    W.set_option("host_chunk_mb", 1)
+    try:
+        _host_vs_oracle(wire, so2, sl2, 8, "unordered")
+    finally:
+        W.set_option("host_chunk_mb", 64)

@@ -1,5 +1,6 @@
 // ws_api.hip — C ABI of the batch decode (include/wsframe_amd.h Part 2):
-// argument checks, per-device workspace, variant dispatch, host-buffer path.
+// argument checks, per-device workspace, variant dispatch (host-buffer path:
+// ws_hostpath.hip).
 //
 // Default path = ws_walker.hip (one wave walks and unmasks one rx segment; fastest
 // measured so far). Variants kept for A/B measurement: "segblock" =
@@ -12,6 +13,7 @@
 
 static __thread char g_last_error[256];
 extern int ws_dbg_flags;
+extern size_t ws_host_chunk_bytes;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -48,6 +50,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "dyn")) g_tune.dyn = (int)value;
     else if (!strcmp(name, "unroll")) g_tune.unroll = (int)value;
     else if (!strcmp(name, "blocks_per_cu")) g_tune.blocks_per_cu = (int)value;
+    else if (!strcmp(name, "host_chunk_mb") && value > 0) ws_host_chunk_bytes = (size_t)value << 20;
     else return -1;
     return 0;
 }
@@ -133,57 +136,3 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char*
     u32* nwork = ds->ws + ((nslots + 63) & ~(size_t)63);
     return ws_launch_split(L, t.split_cfg, t.nt, keys, nwork);
 }
-
-// ---------------------------------------------------------------------------------------------
-// host-buffer entry point: pinned staging + H2D + kernel + D2H (synchronous)
-
-extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
-                                                                const u64* h_seg_off, const u64* h_seg_len,
-                                                                unsigned int nseg, unsigned int max_frames,
-                                                                WebsocketFrameDesc_t* h_desc,
-                                                                WebsocketSegResult_t* h_res, int device) {
-    hipError_t e;
-    unsigned char* d_buf = nullptr;
-    u64 *d_off = nullptr, *d_len = nullptr;
-    WebsocketFrameDesc_t* d_desc = nullptr;
-    WebsocketSegResult_t* d_res = nullptr;
-    hipStream_t st = nullptr;
-    int rc = 0;
-    const size_t ndesc = (size_t)nseg * max_frames;
-    if (nseg == 0) return 0;
-    if ((e = hipSetDevice(device)) != hipSuccess) return ws_set_err("hipSetDevice", e);
-#define WS_TRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = ws_set_err(what, e); goto out; } } while (0)
-    WS_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    WS_TRY(hipMalloc(&d_buf, buflen + WEBSOCKET_BATCH_PAD), "hipMalloc(buf)");
-    WS_TRY(hipMemsetAsync(d_buf + buflen, 0, WEBSOCKET_BATCH_PAD, st), "hipMemset(pad)");
-    WS_TRY(hipMalloc(&d_off, nseg * sizeof(u64)), "hipMalloc(seg_off)");
-    WS_TRY(hipMalloc(&d_len, nseg * sizeof(u64)), "hipMalloc(seg_len)");
-    WS_TRY(hipMalloc(&d_desc, (ndesc ? ndesc : 1) * sizeof(WebsocketFrameDesc_t)), "hipMalloc(desc)");
-    WS_TRY(hipMalloc(&d_res, nseg * sizeof(WebsocketSegResult_t)), "hipMalloc(res)");
-    WS_TRY(hipMemcpyAsync(d_buf, h_buf, buflen, hipMemcpyHostToDevice, st), "H2D buf");
-    WS_TRY(hipMemcpyAsync(d_off, h_seg_off, nseg * sizeof(u64), hipMemcpyHostToDevice, st), "H2D seg_off");
-    WS_TRY(hipMemcpyAsync(d_len, h_seg_len, nseg * sizeof(u64), hipMemcpyHostToDevice, st), "H2D seg_len");
-    rc = websocketframeBatchDecodeDevice(d_buf, d_off, d_len, nseg, max_frames, nullptr, d_desc, d_res, st);
-    if (rc) goto out;
-    WS_TRY(hipMemcpyAsync(h_buf, d_buf, buflen, hipMemcpyDeviceToHost, st), "D2H buf");
-    WS_TRY(hipMemcpyAsync(h_res, d_res, nseg * sizeof(WebsocketSegResult_t), hipMemcpyDeviceToHost, st), "D2H res");
-    WS_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
-    // descriptors: copy only the used prefix of every segment's slots
-    for (u32 s = 0; s < nseg; ++s) {
-        if (h_res[s].n_frames)
-            WS_TRY(hipMemcpyAsync(h_desc + (size_t)s * max_frames, d_desc + (size_t)s * max_frames,
-                                  h_res[s].n_frames * sizeof(WebsocketFrameDesc_t), hipMemcpyDeviceToHost, st),
-                   "D2H desc");
-    }
-    WS_TRY(hipStreamSynchronize(st), "hipStreamSynchronize");
-#undef WS_TRY
-out:
-    if (d_buf) (void)hipFree(d_buf);
-    if (d_off) (void)hipFree(d_off);
-    if (d_len) (void)hipFree(d_len);
-    if (d_desc) (void)hipFree(d_desc);
-    if (d_res) (void)hipFree(d_res);
-    if (st) (void)hipStreamDestroy(st);
-    return rc;
-}
-
