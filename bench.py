@@ -25,8 +25,10 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
-KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel"}
-DEFAULT_PATH = 1
+KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel", 3: "ws_piece_unmask_kernel"}
+STEP_KERNELS = {3: "hipMemsetAsync(piece table) + ws_piece_walk_kernel + ws_piece_unmask_kernel + gated "
+                   "ws_walker_kernel (exits at once for ordered segments)"}
+DEFAULT_PATH = 3
 
 
 def pmc_traffic(kernel, algo_bytes):
@@ -340,6 +342,9 @@ def main():
                      "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
                      "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
                      "kernel": KERNELS[path], "algo_bytes_per_launch": wl.algo_bytes,
+                     "timed": "HIP events around each decode call on its stream: " +
+                              STEP_KERNELS.get(path, KERNELS[path]),
+                     "per_kernel_ns": pmc[1].get("per_kernel_avg_ns") if pmc else None,
                      "kernel_ms_mean": round(mean_kern * 1e3, 4), "kernel_ms_min": round(float(kern_ms.min()), 4)},
         "verified": mism == 0,
         "cpu_baseline": None,

@@ -111,7 +111,10 @@ typedef struct WebsocketSegResult_t {
 /* Decode a device-resident batch of rx segments in place, asynchronously on
  * `hip_stream` (hipStream_t, NULL = default stream).
  *   d_buf          batch buffer (device); payloads are unmasked in place
- *   d_seg_off/len  nseg segments [off, off+len) of d_buf (device arrays); must not overlap
+ *   buflen         every segment lies in [0, buflen) of d_buf; d_buf[0, buflen + WEBSOCKET_BATCH_PAD)
+ *                  must be readable (the kernels read, never write, bytes outside segments)
+ *   d_seg_off/len  nseg segments [off, off+len) of d_buf (device arrays); must not overlap;
+ *                  ascending order is fastest (any order is decoded correctly)
  *   max_frames     descriptor capacity per segment (>= 1)
  *   d_desc_base    optional (device, may be NULL): first descriptor slot of segment s;
  *                  NULL means s * max_frames
@@ -122,7 +125,8 @@ typedef struct WebsocketSegResult_t {
  *                                if (r < 0) error; if (r == 0) break; off += r; }
  * (net_reactor.c:515-526), including every reference quirk (§SURVEY 4).
  * Returns 0, or a negative code if the launch failed (see websocketframeGpuLastError). */
-WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, const unsigned long long* d_seg_off,
+WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, unsigned long long buflen,
+                                                       const unsigned long long* d_seg_off,
                                                        const unsigned long long* d_seg_len, unsigned int nseg,
                                                        unsigned int max_frames,
                                                        const unsigned long long* d_desc_base,

@@ -259,3 +259,28 @@ def test_host_path_unordered_segments(dev):
         _host_vs_oracle(wire, so2, sl2, 8, "unordered")
     finally:
         W.set_option("host_chunk_mb", 64)
+
+
+def test_device_unordered_and_out_of_range(dev):
+    """segments out of buffer order, and a batch whose declared length is short of the last
+    segment: decoded correctly either way (the piece path hands such batches to the walker)"""
+    rng = np.random.default_rng(13)
+    wire, so, sl = random_stream(rng, 600)
+    perm = rng.permutation(len(so))
+    assert_same(dev, wire, [so[i] for i in perm], [sl[i] for i in perm], 8, tag="unordered")
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    d[:n] = torch.from_numpy(wire).to(dev)
+    so_t = torch.tensor(np.asarray(so, dtype=np.int64), device=dev)
+    sl_t = torch.tensor(np.asarray(sl, dtype=np.int64), device=dev)
+    desc = torch.zeros(len(so) * 8 * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
+    lib = W.load_lib()
+    rc = lib.websocketframeBatchDecodeDevice(d.data_ptr(), max(0, n - 100), so_t.data_ptr(), sl_t.data_ptr(), len(so), 8,
+                                             None, desc.data_ptr(), res.data_ptr(), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, so, sl, 8)
+    assert np.array_equal(res.cpu().numpy().view(W.SEGRES_DTYPE), orr)
+    assert np.array_equal(d[:n].cpu().numpy(), ob)

@@ -32,7 +32,8 @@ def main():
                  28: "buf128x4_nt", 29: "buf64x4_nt", 5: "rounds1", 4: "oneshot",
                  40: "ldspipe512x6_c3", 41: "ldspipe512x8_c3", 42: "ldspipe256x12_c3", 43: "ldspipe1024x3_c3",
                  44: "ldspipe512x6_c1", 45: "ldspipe512x6_c7", 46: "ldspipe256x8_c3", 47: "ldspipe512x6_il",
-                 48: "ldspipe256x8_il", 49: "ldspipe1024x3_il"}
+                 48: "ldspipe256x8_il", 49: "ldspipe1024x3_il", 60: "dep256x4_d0", 61: "dep256x4_d1",
+                 62: "dep256x4_d2", 63: "dep256x4_d4", 64: "dep256x8_d2", 65: "dep512x8_d2"}
         res = {}
         for r in range(3):
             for spec in args.modes.split(","):

@@ -1,6 +1,8 @@
 """Summarise a rocprofv3 run of bench.py into profiles/ (committed evidence).
 
-    python tools/prof_summary.py gpurun_out/r01 r01 [--kernel ws_walker_kernel]
+    python tools/prof_summary.py gpurun_out/r01 r01 [--kernel ws_piece_unmask_kernel,ws_piece_walk_kernel]
+
+The first --kernel name is the dominant kernel; traffic per step sums every listed kernel.
 
 Inputs (written by tools/profile.sh on the GPU box):
   <dir>/trace/run_kernel_stats.csv       rocprofv3 --kernel-trace --stats
@@ -31,13 +33,30 @@ def per_launch(path, kernel, counter):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    kernel = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "ws_walker_kernel"
+    names = (sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv
+             else "ws_piece_unmask_kernel,ws_piece_walk_kernel").split(",")
+    kernel = names[0]
     out = os.path.join(REPO, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, tag + "_kernel_stats.csv"))
-    stats = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))) if kernel in r["Name"]]
-    fetch_kib, nf = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kernel, "FETCH_SIZE")
-    write_kib, nw = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kernel, "WRITE_SIZE")
+    rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    stats = [r for r in rows if kernel in r["Name"]]
+    per_kernel = {}
+    fetch_kib = write_kib = 0.0
+    nf = nw = 0
+    for k in names:
+        st = [r for r in rows if k in r["Name"]]
+        f, a = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), k, "FETCH_SIZE")
+        w, b = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), k, "WRITE_SIZE")
+        per_kernel[k] = {"avg_ns": float(st[0]["AverageNs"]) if st else None, "calls": int(st[0]["Calls"]) if st else 0,
+                         "fetch_kib": f, "write_kib": w}
+        if f is None or w is None:
+            fetch_kib = write_kib = None
+        elif fetch_kib is not None:
+            fetch_kib += f
+            write_kib += w
+        if k == kernel:
+            nf, nw = a, b
     bench = json.load(open(os.path.join(src, "bench.json")))
     algo = bench["roofline"]["algo_bytes_per_launch"]
     rec = {
@@ -46,6 +65,9 @@ def main():
         "rocprof_avg_ns": float(stats[0]["AverageNs"]) if stats else None,
         "rocprof_min_ns": float(stats[0]["MinNs"]) if stats else None,
         "bench_kernel_ms_mean": bench["roofline"]["kernel_ms_mean"],
+        "kernels_summed": names,
+        "per_kernel": per_kernel,
+        "per_kernel_avg_ns": {k: v["avg_ns"] for k, v in per_kernel.items()},
         "fetch_size_kib_per_launch": fetch_kib, "fetch_dispatches": nf,
         "write_size_kib_per_launch": write_kib, "write_dispatches": nw,
         "fetch_bytes_corrected": 2 * fetch_kib * 1024 if fetch_kib is not None else None,

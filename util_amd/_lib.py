@@ -66,7 +66,7 @@ def load_lib():
     lib.websocketframeFreeString.restype = None
     lib.websocketframeFreeString.argtypes = [vp]
     lib.websocketframeBatchDecodeDevice.restype = i32
-    lib.websocketframeBatchDecodeDevice.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp]
+    lib.websocketframeBatchDecodeDevice.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, vp, vp]
     lib.websocketframeBatchDecodeHost.restype = i32
     lib.websocketframeBatchDecodeHost.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, i32]
     lib.websocketframeGpuLastError.restype = C.c_char_p

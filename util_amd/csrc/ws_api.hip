@@ -2,10 +2,11 @@
 // argument checks, per-device workspace, variant dispatch (host-buffer path:
 // ws_hostpath.hip).
 //
-// Default path = ws_walker.hip (one wave walks and unmasks one rx segment; fastest
-// measured so far). Variants kept for A/B measurement: "segblock" =
-// ws_segblock.hip (one workgroup per segment, one load round), "split" =
-// ws_split.hip (walk kernel + unmask kernel).
+// Default path 3 = ws_piece.hip (walk kernel + one-shot unmask over 16 KiB pieces;
+// fastest measured). Variants kept for A/B measurement: 1 "walker" =
+// ws_walker.hip (one wave walks and unmasks one segment; also the gated fallback of
+// path 3 for unordered segments), 0 "segblock" = ws_segblock.hip (one workgroup per
+// segment), 2 "split" = ws_split.hip (walk kernel + one block per segment).
 #include <stdio.h>
 #include <string.h>
 
@@ -31,7 +32,8 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 // launch configuration (tunable for in-process A/B by bench/profiling tools)
 
 struct WsTuning {
-    int path = 1;           // 0: segment blocks (ws_segblock), 1: fused walker, 2: split walk + unmask
+    int path = 3;           // 0: segment blocks (ws_segblock), 1: fused walker, 2: split walk + unmask,
+                            // 3: walk + one-shot 16 KiB pieces (ws_piece)
     int seg_cfg = 0;        // segment-block geometry: 0 256x17, 1 512x9, 2 1024x5, 3 256x8, 4 512x4
     int split_cfg = 0;      // split unmask geometry: 0 512x9, 1 1024x5, 2 256x17, 3 512x4
     int nt = 1;             // 0 plain, 1 nontemporal loads+stores, 2 nontemporal stores only
@@ -106,13 +108,18 @@ static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream) {
     return 0;
 }
 
-extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, const u64* d_seg_off,
-                                                                  const u64* d_seg_len, unsigned int nseg,
-                                                                  unsigned int max_frames, const u64* d_desc_base,
-                                                                  WebsocketFrameDesc_t* d_desc,
-                                                                  WebsocketSegResult_t* d_res, void* hip_stream) {
+size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
+    const WsTuning t = g_tune;
+    if (t.path == 3) return ws_piece_workspace_bytes(span, nseg, max_frames);
+    if (t.path == 2) return (size_t)nseg * max_frames * 4 + (size_t)nseg * 4 + 256 + 256;
+    return 0;
+}
+
+int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, const u64* d_seg_len, u32 nseg,
+                    u32 max_frames, const u64* d_desc_base, WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
+                    hipStream_t stream, void* ws, size_t ws_bytes) {
     if (nseg == 0) return 0;
-    if (!d_buf || !d_seg_off || !d_seg_len || !d_desc || !d_res || max_frames == 0)
+    if (!d_buf || !d_seg_off || !d_seg_len || !d_desc || !d_res || max_frames == 0 || hi < lo)
         return ws_set_msg("websocketframeBatchDecodeDevice: invalid argument");
     if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_res)) & 15)
         return ws_set_msg("websocketframeBatchDecodeDevice: d_desc/d_res not 16-B aligned");
@@ -123,16 +130,34 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char*
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg; L.max_frames = max_frames;
     L.desc_base = d_desc_base; L.desc = d_desc; L.res = d_res;
-    L.stream = reinterpret_cast<hipStream_t>(hip_stream);
+    L.stream = stream;
     L.cus = ds->cus;
+    u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
     if (t.path == 0) return ws_launch_segblock(L, t.seg_cfg, t.nt);
-    if (t.path == 1) {
-        u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
-        return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
+    if (t.path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
+    const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
+    if (ws && ws_bytes < need) return ws_set_msg("websocketframe batch decode: workspace too small");
+    if (!ws && need) {
+        if ((rc = workspace(ds, need, L.stream))) return rc;
+        ws = ds->ws;
+    }
+    if (t.path == 3) {
+        const u32* ordered = nullptr;
+        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), &ordered))) return rc;
+        // fallback for segments out of buffer order: a small gated walker grid (exits at once otherwise)
+        return ws_launch_walker(L, t.unroll, t.nt, 0, 4, ctr, ordered);
     }
     const size_t nslots = (size_t)nseg * max_frames;
-    if ((rc = workspace(ds, nslots * 4 + (size_t)nseg * 4 + 256, L.stream))) return rc;
-    u32* keys = ds->ws;
-    u32* nwork = ds->ws + ((nslots + 63) & ~(size_t)63);
+    u32* keys = reinterpret_cast<u32*>(ws);
+    u32* nwork = keys + ((nslots + 63) & ~(size_t)63);
     return ws_launch_split(L, t.split_cfg, t.nt, keys, nwork);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, unsigned long long buflen,
+                                                                  const u64* d_seg_off, const u64* d_seg_len,
+                                                                  unsigned int nseg, unsigned int max_frames,
+                                                                  const u64* d_desc_base, WebsocketFrameDesc_t* d_desc,
+                                                                  WebsocketSegResult_t* d_res, void* hip_stream) {
+    return ws_decode_range(d_buf, 0, buflen, d_seg_off, d_seg_len, nseg, max_frames, d_desc_base, d_desc, d_res,
+                           reinterpret_cast<hipStream_t>(hip_stream));
 }

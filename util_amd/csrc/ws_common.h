@@ -214,6 +214,16 @@ struct WsLaunch {
     hipStream_t stream;
     int cus;
 };
-int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr);
+int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr,
+                     const u32* gate = nullptr);
+size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, const u32** ordered_out);
+// the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
+// (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes, else the
+// per-device one is used (concurrent calls on one device must then not overlap)
+int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, const u64* seg_len, u32 nseg,
+                    u32 max_frames, const u64* desc_base, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res,
+                    hipStream_t stream, void* ws = nullptr, size_t ws_bytes = 0);
+size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 int ws_launch_split(const WsLaunch& L, int variant, int nt, u32* keys, u32* nwork);
 int ws_launch_segblock(const WsLaunch& L, int cfg, int nt);

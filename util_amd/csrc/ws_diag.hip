@@ -229,6 +229,37 @@ __global__ __launch_bounds__(64 * (NC + 1)) void ws_calib_ldspipe_kernel(gu32x4*
     }
 }
 
+// mode 60+: one-shot in-place XOR blocks that also resolve a dependent lookup chain of
+// depth DEP (each link a 16-B load whose address depends on the previous one; the
+// last gives the XOR key) while their payload loads are in flight: what a one-shot
+// unmask block pays to find its frame's key from a precomputed table. The table is
+// the other buffer (d_b), read-only.
+template <int T, int U, int DEP>
+__global__ __launch_bounds__(T) void ws_calib_dep_kernel(gu32x4* __restrict__ a, const gu32x4* __restrict__ tbl,
+                                                         u64 n, u64 ntbl) {
+    const u64 i = (u64)blockIdx.x * (T * U) + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16<1>(a + min(i + (u64)T * u, n - 1));
+    u32 idx = blockIdx.x;
+#pragma unroll
+    for (int d = 0; d < DEP; ++d) {
+        const u32x4 t = tbl[(idx * 2654435761u + d) % ntbl];
+        idx = t.x ^ t.y;
+    }
+    const u32 key = idx | 1u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + (u64)T * u < n) st16<1>(v[u] ^ key, a + i + (u64)T * u);
+}
+
+template <int T, int U, int DEP>
+static void cal_dep(gu32x4* a, gu32x4* b, u64 n, hipStream_t st) {
+    const u64 per = (u64)T * U;
+    hipLaunchKernelGGL((ws_calib_dep_kernel<T, U, DEP>), dim3((u32)((n + per - 1) / per)), dim3(T), 0, st, a, b, n,
+                       (u64)(1u << 20));
+}
+
 template <int S, int D, int NC, bool IL = false>
 static void cal_ldspipe(gu32x4* a, u64 n, int blocks, hipStream_t st) {
     hipLaunchKernelGGL((ws_calib_ldspipe_kernel<S, D, NC, IL>), dim3(blocks), dim3(64 * (NC + 1)), 0, st, a, n / S,
@@ -262,6 +293,19 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         else hipLaunchKernelGGL((ws_calib_oneshot_kernel<0>), dim3((u32)nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_oneshot_kernel launch", e);
+    }
+    if (mode >= 60) {  // one-shot + dependent lookups (d_b must hold >= 16 MiB)
+        switch (mode) {
+        case 60: cal_dep<256, 4, 0>(a, b, n, st); break;
+        case 61: cal_dep<256, 4, 1>(a, b, n, st); break;
+        case 62: cal_dep<256, 4, 2>(a, b, n, st); break;
+        case 63: cal_dep<256, 4, 4>(a, b, n, st); break;
+        case 64: cal_dep<256, 8, 2>(a, b, n, st); break;
+        case 65: cal_dep<512, 8, 2>(a, b, n, st); break;
+        default: return ws_set_msg("websocketframeGpuCalibrate: unknown mode");
+        }
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_dep_kernel launch", e);
     }
     if (mode >= 40) {  // LDS pipeline; n must be a multiple of the stage size (1024 chunks covers all)
         switch (mode) {

@@ -26,6 +26,8 @@ struct WsHostSlot {
     size_t desc_cap = 0;
     WebsocketSegResult_t* res = nullptr;
     size_t res_cap = 0;
+    unsigned char* ws = nullptr;   // decode workspace of this slot's stream
+    size_t ws_cap = 0;
 };
 
 struct WsHostPipe {
@@ -114,6 +116,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
         if ((rc = grow(&S.segs, &S.seg_cap, 2 * max_nseg, "hipMalloc(host slot segs)"))) return rc;
         if ((rc = grow(&S.desc, &S.desc_cap, max_nseg * max_frames, "hipMalloc(host slot desc)"))) return rc;
         if ((rc = grow(&S.res, &S.res_cap, max_nseg, "hipMalloc(host slot res)"))) return rc;
+        const size_t wsb = ws_decode_workspace_bytes(max_span, (u32)max_nseg, max_frames);
+        if (wsb && (rc = grow(&S.ws, &S.ws_cap, wsb, "hipMalloc(host slot workspace)"))) return rc;
     }
 #define WS_TRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = ws_set_err(what, e); goto drain; } } while (0)
     for (size_t gi = 0; gi < groups.size(); ++gi) {
@@ -128,8 +132,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
         WS_TRY(hipMemcpyAsync(S.segs + S.seg_cap / 2, h_seg_len + g.s0, n * sizeof(u64), hipMemcpyHostToDevice, S.st),
                "H2D seg_len");
         WS_TRY(hipMemsetAsync(S.desc, 0, nd * sizeof(WebsocketFrameDesc_t), S.st), "hipMemset(desc)");
-        rc = websocketframeBatchDecodeDevice(S.buf - g.lo, S.segs, S.segs + S.seg_cap / 2, n, max_frames, nullptr,
-                                             S.desc, S.res, S.st);
+        rc = ws_decode_range(S.buf - g.lo, g.lo, g.hi, S.segs, S.segs + S.seg_cap / 2, n, max_frames, nullptr, S.desc,
+                             S.res, S.st, S.ws, S.ws_cap);
         if (rc) goto drain;
         WS_TRY(hipMemcpyAsync(h_buf + g.lo, S.buf, span, hipMemcpyDeviceToHost, S.st), "D2H batch");
         WS_TRY(hipMemcpyAsync(h_desc + (size_t)g.s0 * max_frames, S.desc, nd * sizeof(WebsocketFrameDesc_t),

@@ -1,0 +1,250 @@
+// ws_piece.hip — decode as "walk, then one-shot unmask over fixed 16 KiB pieces".
+//
+// The streaming ceiling of this part for an in-place read+write is reached only by
+// ONE-SHOT waves (load once, store once, exit): every persistent pattern measured
+// stays near 5.0–5.5 TB/s, while one-shot 256x4 blocks reach 5.9–6.1 TB/s, even
+// with a chain of 4 dependent table lookups resolved while their payload loads are
+// in flight (tools/calib.py modes 4, 5, 40-49, 60-65).
+//
+// K1 ws_piece_walk_kernel — one LANE per rx segment runs the reactor loop
+//   (net_reactor.c:515-526) over websocketframeDecode's header logic
+//   (websocketframe.c:112-165, ws_parse). Writes the descriptors and segment result,
+//   one payload item per frame (origin-relative [P0, P1) + pre-rotated key, indexed
+//   like the descriptor slot s*max_frames + k), the item count per segment, and for
+//   every 16 KiB piece whose first byte lies in this segment's ownership range
+//   [end of segment s-1, end of segment s) the first item that can touch it.
+//   A segment that starts before the previous one ends (or lies outside [lo, hi))
+//   clears the "ordered" flag.
+// K2 ws_piece_unmask_kernel — one 256-thread block per piece, 4 chunks per lane:
+//   payload loads first, then (while they are in flight) the piece pointer and the
+//   items it leads to (64 per load, hopping to the next segment when the piece
+//   extends past the current one), XOR masks accumulated per chunk, one 16-B store
+//   per fully covered chunk, exact byte stores at payload edges. Every piece is
+//   touched by exactly one block, so no byte is stored twice.
+// Fallback: if the segments are not in ascending buffer order, K2 stores nothing and a
+//   gated walker (ws_walker.hip) decodes the batch.
+#include "ws_common.h"
+
+#define PIECE_T 256
+#define PIECE_U 4
+#define PIECE_SHIFT 14                      // 16 KiB = PIECE_T * PIECE_U * 16 B
+#define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
+#define PWALK_T 256
+
+// item: w0 = P0 | rkey[15:0] << 48, w1 = P1 | rkey[31:16] << 48 (origin-relative bytes < 2^48)
+__device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
+    const u64 w0 = p0 | ((u64)(rk & 0xFFFFu) << 48), w1 = p1 | ((u64)(rk >> 16) << 48);
+    u32x4 q;
+    q.x = (u32)w0; q.y = (u32)(w0 >> 32); q.z = (u32)w1; q.w = (u32)(w1 >> 32);
+    *it = q;
+}
+
+// pieces (index >= pbase) whose first byte is in [lo, hi) (origin-relative) get `val`
+__device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 lo, u64 hi, u64 val) {
+    u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
+    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi; ++p) *gptr<u64>(ptr + (p - pbase)) = val;
+}
+
+__global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned char* __restrict__ buf,
+                                                                 const u64* __restrict__ seg_off,
+                                                                 const u64* __restrict__ seg_len, u32 nseg,
+                                                                 u32 max_frames, const u64* __restrict__ desc_base,
+                                                                 WebsocketFrameDesc_t* __restrict__ desc,
+                                                                 WebsocketSegResult_t* __restrict__ res,
+                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
+                                                                 u64* __restrict__ ptr, u32* __restrict__ ordered,
+                                                                 u64 pbase, u64 lo, u64 hi) {
+    const u32 s = blockIdx.x * PWALK_T + threadIdx.x;
+    if (s >= nseg) return;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const u64 so = seg_off[s], sl = seg_len[s];
+    const u64 prev_end = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
+    // out of order, or outside the declared range: the gated walker decodes the batch instead
+    if (prev_end > so || so < lo || sl > hi - so) atomicAnd(ordered, 0u);
+    const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
+    const u64 ibase = (u64)s * max_frames;
+    const u64 sorg = so + lead0;                                            // origin-relative segment start
+    const u64 tag = (u64)s << 32;
+    put_ptrs(ptr, pbase, s ? prev_end + lead0 : 0, sorg, tag);                     // pieces starting in the gap before s
+    u64 off = 0, walked_end = sorg;
+    u32 nf = 0, extra = 0;
+    int status = WEBSOCKET_SEG_OK;
+    uintptr_t p = reinterpret_cast<uintptr_t>(buf + so);
+    u32x4 x0 = reinterpret_cast<const gu32x4*>(p & ~(uintptr_t)15)[0];
+    u32x4 x1 = reinterpret_cast<const gu32x4*>(p & ~(uintptr_t)15)[1];
+    while (off < sl) {
+        if (nf >= max_frames) { status = WEBSOCKET_SEG_MAX_FRAMES; break; }
+        const u64 avail = sl - off;
+        if (avail < 2) break;                                                // websocketframe.c:121
+        u64 h0, h1;
+        ws_hdr_from32(x0, x1, (u32)(p & 15), h0, h1);
+        const WsHdr h = ws_parse(h0, h1, avail);
+        if (h.kind == WS_PARSE_INCOMPLETE) break;
+        if (h.kind == WS_PARSE_WRAP) { status = WEBSOCKET_SEG_ERR_LEN_WRAP; break; }
+        // next header's loads issue before this frame's stores (vmcnt retires in order)
+        const uintptr_t pn = h.ret > 0 && off + (u32)h.ret < sl ? p + (u32)h.ret : p;
+        const gu32x4* qn = reinterpret_cast<const gu32x4*>(pn & ~(uintptr_t)15);
+        x0 = qn[0];
+        x1 = qn[1];
+        const u64 fo = sorg + off;                                           // frame start (origin-relative)
+        const u64 p0 = fo + h.hdr;
+        walked_end = p0 + h.plen;                                            // frame extent (ret may truncate)
+        // item k = nf: the payload range if masked, else an empty range at the payload start
+        put_item(gptr<u32x4>(items + ibase + nf), p0, h.masked ? walked_end : p0, rotl32(h.key, 8u * (u32)(p0 & 3)));
+        put_ptrs(ptr, pbase, fo, walked_end, tag | nf);                             // pieces starting inside this frame
+        if (h.ret == 0) { extra = 1; break; }                                // (int) truncated to 0: unmasked,
+        ws_store_desc(desc + dbase + nf, so + off, h);                       // no descriptor, loop breaks
+        ++nf;
+        if (h.ret < 0) { status = WEBSOCKET_SEG_ERR_DECODE; break; }         // net_reactor.c:518-520
+        off += (u32)h.ret;                                                   // net_reactor.c:525
+        p = pn;
+    }
+    const u32 cnt = nf + extra;
+    put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);                         // pieces starting in the tail
+    ws_store_res(res + s, off, nf, status);
+    *gptr<u32>(nwork + s) = cnt;
+}
+
+template <int NT>
+__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
+                                                                  const u64* __restrict__ seg_off,
+                                                                  const u64* __restrict__ seg_len, u32 nseg,
+                                                                  u32 max_frames, const u32x4* __restrict__ items,
+                                                                  const u32* __restrict__ nwork,
+                                                                  const u64* __restrict__ ptr,
+                                                                  const u32* __restrict__ ordered, u64 pbase,
+                                                                  u64 c_lo, u64 c_hi) {
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u64 pc0 = (pbase + blockIdx.x) << (PIECE_SHIFT - 4);              // first chunk of the piece
+    const u64 wc0 = pc0 + (u64)wv * (64 * PIECE_U);                          // this wave's 4 KiB: 256 chunks
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
+    // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
+    u32x4 v[PIECE_U];
+#pragma unroll
+    for (int u = 0; u < PIECE_U; ++u) {
+        const u64 c = wc0 + (u64)(u * 64 + lane);
+        v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
+    }
+    // ---- 2. items that touch this wave's range [r0, r1) (origin-relative bytes)
+    const u64 r0 = wc0 << 4, r1 = r0 + 64 * PIECE_U * 16;
+    const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+        reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
+    const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ordered));
+    u32 m[PIECE_U][4];
+    u32 cov[PIECE_U];
+#pragma unroll
+    for (int u = 0; u < PIECE_U; ++u) { m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0; cov[u] = 0; }
+    if (!ok || pv == PIECE_NONE) return;
+    u32 s = (u32)(pv >> 32), k = (u32)pv;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    for (;;) {
+        const u32 cnt = nwork[s];
+        if (k < cnt) {
+            const u32 j = k + lane;
+            u32x4 q = {0, 0, 0, 0};
+            if (j < cnt) q = items[(u64)s * max_frames + j];
+            const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
+            const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
+            const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
+            const bool valid = j < cnt;
+            // items are in address order: the first one starting at/after r1 ends the scan
+            const u64 past = __ballot(valid && P0 >= r1);
+            const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
+            const u64 hit = __ballot(valid && lane < nlim && P1 > r0 && P0 < P1);
+            u64 hm = hit;
+            while (hm) {
+                const int i = __builtin_ctzll(hm);
+                hm &= hm - 1;
+                const long long a = (long long)((u64)(u32)__builtin_amdgcn_readlane((int)(u32)P0, i) |
+                                                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(P0 >> 32), i) << 32));
+                const long long b = (long long)((u64)(u32)__builtin_amdgcn_readlane((int)(u32)P1, i) |
+                                                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(P1 >> 32), i) << 32));
+                const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
+#pragma unroll
+                for (int u = 0; u < PIECE_U; ++u) {
+                    const long long x = (long long)((wc0 + (u64)(u * 64 + lane)) << 4);
+                    const long long lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
+                    if (hi <= lo) continue;
+                    const u32 bits = (0xFFFFu >> (16 - (int)hi)) & (0xFFFFu << (int)lo);
+                    cov[u] |= bits;
+                    m[u][0] |= key & nib_to_bytemask(bits & 15u);
+                    m[u][1] |= key & nib_to_bytemask((bits >> 4) & 15u);
+                    m[u][2] |= key & nib_to_bytemask((bits >> 8) & 15u);
+                    m[u][3] |= key & nib_to_bytemask(bits >> 12);
+                }
+            }
+            if (nlim < 64) break;                                           // reached an item past the range
+            if (k + 64 < cnt) { k += 64; continue; }                        // more items of this segment
+        }
+        // this segment has no more items: continue with the next one if it starts in range
+        if (++s >= nseg) break;
+        if (seg_off[s] + lead0 >= r1) break;
+        k = 0;
+    }
+    // ---- 3. store: full chunks one 16-B store, edge chunks exactly the covered bytes
+#pragma unroll
+    for (int u = 0; u < PIECE_U; ++u) {
+        const u64 c = wc0 + (u64)(u * 64 + lane);
+        if (!cov[u] || c < c_lo || c >= c_hi) continue;
+        u32x4 w = v[u];
+        w.x ^= m[u][0]; w.y ^= m[u][1]; w.z ^= m[u][2]; w.w ^= m[u][3];
+        if (cov[u] == 0xFFFFu) {
+            st16<NT>(w, base + c);
+        } else {
+            gu8* const pb = reinterpret_cast<gu8*>(base + c);
+#pragma unroll
+            for (u32 q = 0; q < 16; ++q) {
+                const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
+                if ((cov[u] >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
+            }
+        }
+    }
+}
+
+// ws layout: [ordered u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
+static u64 piece_count(u64 lo_org, u64 hi_org) {
+    return hi_org > lo_org ? ((hi_org - 1) >> PIECE_SHIFT) - (lo_org >> PIECE_SHIFT) + 1 : 0;
+}
+
+size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
+    const u64 npieces = (span + 15) / (1ull << PIECE_SHIFT) + 2;
+    size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
+    b = (b + (size_t)nseg * 4 + 15) & ~(size_t)15;
+    return b + (size_t)nseg * max_frames * 16 + 16;
+}
+
+// Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *ordered_out = the flag a gated
+// fallback walker must test.
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, const u32** ordered_out) {
+    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
+    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
+    const u64 npieces = piece_count(lo_org, hi_org);
+    const u64 pbase = lo_org >> PIECE_SHIFT;
+    const u64 c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
+    u32* ordered = reinterpret_cast<u32*>(ws);
+    u64* ptr = reinterpret_cast<u64*>(ws + 16);
+    size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
+    u32* nwork = reinterpret_cast<u32*>(ws + b);
+    b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
+    u32x4* items = reinterpret_cast<u32x4*>(ws + b);
+    hipError_t e = hipMemsetAsync(ws, 0xFF, 16 + npieces * 8, L.stream);    // ordered = ~0, ptr = PIECE_NONE
+    if (e != hipSuccess) return ws_set_err("hipMemsetAsync(piece workspace)", e);
+    hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
+                       L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, items, nwork,
+                       ptr, ordered, pbase, lo, hi);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_walk_kernel launch", e);
+    if (npieces) {
+        if (nt == 1)
+            hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
+                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, ordered, pbase, c_lo,
+                               c_hi);
+        else
+            hipLaunchKernelGGL((ws_piece_unmask_kernel<0>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
+                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, ordered, pbase, c_lo,
+                               c_hi);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
+    }
+    *ordered_out = ordered;
+    return 0;
+}

@@ -131,8 +131,10 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
     assert buf.numel() >= BATCH_PAD, "device batch needs WEBSOCKET_BATCH_PAD bytes of slack"
     assert seg_len.numel() == nseg and res.numel() * res.element_size() >= 16 * nseg
     assert buf.is_cuda and seg_off.is_cuda and seg_len.is_cuda and desc.is_cuda and res.is_cuda
-    rc = load_lib().websocketframeBatchDecodeDevice(_ptr(buf), _ptr(seg_off), _ptr(seg_len), nseg, max_frames,
-                                                    _ptr(desc_base), _ptr(desc), _ptr(res), _stream(stream))
+    # buflen: segments lie in [0, numel - PAD); the last PAD bytes are the readable slack
+    rc = load_lib().websocketframeBatchDecodeDevice(_ptr(buf), buf.numel() - BATCH_PAD, _ptr(seg_off), _ptr(seg_len),
+                                                    nseg, max_frames, _ptr(desc_base), _ptr(desc), _ptr(res),
+                                                    _stream(stream))
     check(rc, "websocketframeBatchDecodeDevice")
 
 
