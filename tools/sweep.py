@@ -39,7 +39,8 @@ def main():
     dev = torch.device("cuda:0")
     wl = bench.Workload.make(args.config, dev, nframes=args.frames)
     variants = [parse(v) for v in args.variants]
-    defaults = {"dyn": 1, "unroll": 4, "nt": 1, "blocks_per_cu": 0}
+    # the library defaults (WsTuning in ws_api.hip); every variant starts from these
+    defaults = {"path": 3, "piece_scan": 3, "dyn": 0, "unroll": 4, "nt": 1, "blocks_per_cu": 64}
     times = {i: [] for i in range(len(variants))}
     for r in range(args.rounds):
         for i, v in enumerate(variants):

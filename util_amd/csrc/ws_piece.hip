@@ -105,6 +105,114 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
     *gptr<u32>(nwork + s) = cnt;
 }
 
+// K1, group variant: G lanes (16/32/64) per segment, header walk by STRIDE SPECULATION
+// (as ws_segblock.hip): lane k of the group parses the header at off + k*g (g = the
+// last frame's length); the chain is right up to the first lane whose frame length
+// differs (ballot), so a run of up to G equal frames is walked in one round trip and
+// its items, descriptors and piece pointers are written by the lanes in parallel.
+// Small G keeps more segments in flight per wave (the walk is latency-bound).
+#define PSCAN_T 256
+template <int G>
+__global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned char* __restrict__ buf,
+                                                                const u64* __restrict__ seg_off,
+                                                                const u64* __restrict__ seg_len, u32 nseg,
+                                                                u32 max_frames, const u64* __restrict__ desc_base,
+                                                                WebsocketFrameDesc_t* __restrict__ desc,
+                                                                WebsocketSegResult_t* __restrict__ res,
+                                                                u32x4* __restrict__ items, u32* __restrict__ nwork,
+                                                                u64* __restrict__ ptr, u32* __restrict__ ordered,
+                                                                u64 pbase, u64 lo, u64 hi) {
+    static_assert(G == 16 || G == 32 || G == 64, "group size");
+    const u32 lane = threadIdx.x & 63;
+    const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
+    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / G;
+    bool active = s < nseg;
+    const u32 sc = active ? s : nseg - 1;                                    // inactive groups: harmless loads
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const u64 so = seg_off[sc], sl = seg_len[sc];
+    const u64 prev_end = sc ? seg_off[sc - 1] + seg_len[sc - 1] : 0;
+    if (active && gl == 0 && (prev_end > so || so < lo || sl > hi - so)) atomicAnd(ordered, 0u);
+    const u64 dbase = desc_base ? desc_base[sc] : (u64)sc * max_frames;
+    const u64 ibase = (u64)sc * max_frames;
+    const u64 sorg = so + lead0;
+    const u64 tag = (u64)sc << 32;
+    const uintptr_t seg = reinterpret_cast<uintptr_t>(buf + so);
+    if (active && gl == 0) put_ptrs(ptr, pbase, s ? prev_end + lead0 : 0, sorg, tag);
+    u64 off = 0, g = 0, walked_end = sorg;
+    u32 nf = 0, extra = 0;
+    int status = WEBSOCKET_SEG_OK;
+    const u64 gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+    while (__ballot(active)) {
+        const u64 pos = off + (u64)gl * g;                                  // candidate frame offset
+        const bool cand = active && (gl == 0 || g > 0);
+        const bool eval = cand && pos < sl;
+        const uintptr_t pa = seg + (eval ? pos : 0);
+        const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+        const u32x4 x0 = q[0], x1 = q[1];                                  // WEBSOCKET_BATCH_PAD: readable
+        u64 h0, h1;
+        ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
+        const WsHdr h = ws_parse(h0, h1, eval ? sl - pos : 0);
+        // per-lane outcome in the reactor loop's order (net_reactor.c:515-526):
+        //   0 consumed, chain continues   1 consumed, length != g: step ends
+        //   2 consumed, walk ends (ret <= 0)   3 not consumed, walk ends
+        u32 code = 3;
+        int st = WEBSOCKET_SEG_OK;
+        if (cand) {
+            if (pos >= sl) code = 3;
+            else if (nf + gl >= max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
+            else if (sl - pos < 2) code = 3;                                 // websocketframe.c:121
+            else if (h.kind == WS_PARSE_INCOMPLETE) code = 3;
+            else if (h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
+            else if (h.ret <= 0) { code = 2; st = h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
+            else code = (u64)(u32)h.ret == g ? 0u : 1u;
+        }
+        const u64 stop = (__ballot(code != 0) >> gb) & gmask;
+        const u32 mm = stop ? (u32)__builtin_ctzll(stop) : (u32)G;         // first non-continuing lane
+        const u32 src = gb + (mm < G ? mm : G - 1);
+        const u32 code_m = mm < G ? (u32)__shfl((int)code, (int)src) : 0u;
+        const int ret_m = __shfl(h.ret, (int)src);
+        const int st_m = __shfl(st, (int)src);
+        const u32 ntake = active ? mm + ((code_m == 1 || code_m == 2) ? 1u : 0u) : 0u;
+        const u64 fo = sorg + pos;
+        const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
+        if (gl < ntake) {                                                   // consumed frames, in parallel
+            put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0,
+                     rotl32(h.key, 8u * (u32)(p0 & 3)));
+            put_ptrs(ptr, pbase, fo, fe, tag | (nf + gl));
+            if (h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
+        }
+        const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
+        if (ntake) walked_end = fe_last;
+        if (!active) continue;
+        if (mm == G) {                                                      // the whole step continued
+            nf += G;
+            off += G * g;
+            continue;
+        }
+        const u64 pos_m = off + (u64)mm * g;
+        nf += mm;
+        if (code_m == 1) {                                                  // consumed, new stride
+            nf += 1;
+            off = pos_m + (u32)ret_m;
+            g = (u32)ret_m;
+            continue;
+        }
+        off = pos_m;
+        if (code_m == 2) {
+            if (ret_m != 0) nf += 1;                                        // ret < 0 keeps its descriptor
+            else extra = 1;                                                 // ret == 0: unmasked, not counted
+        }
+        status = st_m;
+        active = false;
+        if (gl == 0) {
+            const u32 cnt = nf + extra;
+            put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);         // pieces starting in the tail
+            ws_store_res(res + s, off, nf, status);
+            *gptr<u32>(nwork + s) = cnt;
+        }
+    }
+}
+
 template <int NT>
 __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
@@ -127,7 +235,8 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
     }
     // ---- 2. items that touch this wave's range [r0, r1) (origin-relative bytes)
-    const u64 r0 = wc0 << 4, r1 = r0 + 64 * PIECE_U * 16;
+    constexpr long long RW = 64 * PIECE_U * 16;                             // this wave's bytes
+    const u64 r0 = wc0 << 4, r1 = r0 + RW;
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
         reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
     const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ordered));
@@ -135,38 +244,39 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     u32 cov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) { m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0; cov[u] = 0; }
-    if (!ok || pv == PIECE_NONE) return;
-    u32 s = (u32)(pv >> 32), k = (u32)pv;
+    // no early return: an exit branch here would be hoisted above the payload loads
+    u32 s = ok && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
-    for (;;) {
+    const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
+    while (s < nseg) {
         const u32 cnt = nwork[s];
         if (k < cnt) {
             const u32 j = k + lane;
+            const bool valid = j < cnt;
             u32x4 q = {0, 0, 0, 0};
-            if (j < cnt) q = items[(u64)s * max_frames + j];
+            if (valid) q = items[(u64)s * max_frames + j];
             const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
             const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
             const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
-            const bool valid = j < cnt;
             // items are in address order: the first one starting at/after r1 ends the scan
             const u64 past = __ballot(valid && P0 >= r1);
             const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
-            const u64 hit = __ballot(valid && lane < nlim && P1 > r0 && P0 < P1);
-            u64 hm = hit;
+            // wave-relative item range, clamped to [-16, RW + 16] (32-bit from here on)
+            const long long ra = (long long)(P0 - r0), rb = (long long)(P1 - r0);
+            const int A = (int)(ra < -16 ? -16 : (ra > RW + 16 ? RW + 16 : ra));
+            const int B = (int)(rb < -16 ? -16 : (rb > RW + 16 ? RW + 16 : rb));
+            u64 hm = __ballot(valid && lane < nlim && P1 > r0 && P0 < P1);
             while (hm) {
                 const int i = __builtin_ctzll(hm);
                 hm &= hm - 1;
-                const long long a = (long long)((u64)(u32)__builtin_amdgcn_readlane((int)(u32)P0, i) |
-                                                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(P0 >> 32), i) << 32));
-                const long long b = (long long)((u64)(u32)__builtin_amdgcn_readlane((int)(u32)P1, i) |
-                                                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(P1 >> 32), i) << 32));
+                const int a = __builtin_amdgcn_readlane(A, i), b = __builtin_amdgcn_readlane(B, i);
                 const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
 #pragma unroll
                 for (int u = 0; u < PIECE_U; ++u) {
-                    const long long x = (long long)((wc0 + (u64)(u * 64 + lane)) << 4);
-                    const long long lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
+                    const int x = u * 1024 + xl;
+                    const int lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
                     if (hi <= lo) continue;
-                    const u32 bits = (0xFFFFu >> (16 - (int)hi)) & (0xFFFFu << (int)lo);
+                    const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
                     cov[u] |= bits;
                     m[u][0] |= key & nib_to_bytemask(bits & 15u);
                     m[u][1] |= key & nib_to_bytemask((bits >> 4) & 15u);
@@ -178,8 +288,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             if (k + 64 < cnt) { k += 64; continue; }                        // more items of this segment
         }
         // this segment has no more items: continue with the next one if it starts in range
-        if (++s >= nseg) break;
-        if (seg_off[s] + lead0 >= r1) break;
+        if (++s >= nseg || seg_off[s] + lead0 >= r1) break;
         k = 0;
     }
     // ---- 3. store: full chunks one 16-B store, edge chunks exactly the covered bytes
@@ -216,6 +325,8 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 
 // Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *ordered_out = the flag a gated
 // fallback walker must test.
+int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3: 64/32/16 lanes per segment
+
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, const u32** ordered_out) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
@@ -230,9 +341,17 @@ int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws
     u32x4* items = reinterpret_cast<u32x4*>(ws + b);
     hipError_t e = hipMemsetAsync(ws, 0xFF, 16 + npieces * 8, L.stream);    // ordered = ~0, ptr = PIECE_NONE
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(piece workspace)", e);
-    hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
-                       L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, items, nwork,
-                       ptr, ordered, pbase, lo, hi);
+    if (ws_piece_scan >= 1 && ws_piece_scan <= 3) {
+        const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : 16);
+        const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
+        auto k = G == 64 ? ws_piece_scan_kernel<64> : (G == 32 ? ws_piece_scan_kernel<32> : ws_piece_scan_kernel<16>);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
+                           L.max_frames, L.desc_base, L.desc, L.res, items, nwork, ptr, ordered, pbase, lo, hi);
+    }
+    else
+        hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, items, nwork,
+                           ptr, ordered, pbase, lo, hi);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_walk_kernel launch", e);
     if (npieces) {
         if (nt == 1)
