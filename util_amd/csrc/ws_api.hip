@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "ws_common.h"
 
 static __thread char g_last_error[256];
@@ -106,6 +108,7 @@ static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream) {
     }
     const size_t sz = bytes + bytes / 4 + 4096;
     if ((e = hipMalloc(&ds->ws, sz)) != hipSuccess) return ws_set_err("hipMalloc(workspace)", e);
+    if ((e = hipMemset(ds->ws, 0, 16)) != hipSuccess) return ws_set_err("hipMemset(workspace)", e);
     ds->ws_bytes = sz;
     return 0;
 }
@@ -144,10 +147,13 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         ws = ds->ws;
     }
     if (t.path == 3) {
-        const u32* ordered = nullptr;
-        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), &ordered))) return rc;
+        static std::atomic<u32> s_gen{0};
+        u32 gen = ++s_gen;
+        if (gen == 0) gen = ++s_gen;                                   // 0 = a fresh workspace's value
+        const u32* disorder = nullptr;
+        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder))) return rc;
         // fallback for segments out of buffer order: a small gated walker grid (exits at once otherwise)
-        return ws_launch_walker(L, t.unroll, t.nt, 0, 4, ctr, ordered);
+        return ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen);
     }
     const size_t nslots = (size_t)nseg * max_frames;
     u32* keys = reinterpret_cast<u32*>(ws);

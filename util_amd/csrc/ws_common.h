@@ -215,12 +215,13 @@ struct WsLaunch {
     int cus;
 };
 int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr,
-                     const u32* gate = nullptr);
+                     const u32* gate = nullptr, u32 gate_gen = 0);
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, const u32** ordered_out);
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
-// (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes, else the
-// per-device one is used (concurrent calls on one device must then not overlap)
+// (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes whose
+// first 16 bytes were zeroed once after allocation, else the per-device one is used
+// (concurrent calls on one device must then not overlap)
 int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, const u64* seg_len, u32 nseg,
                     u32 max_frames, const u64* desc_base, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res,
                     hipStream_t stream, void* ws = nullptr, size_t ws_bytes = 0);

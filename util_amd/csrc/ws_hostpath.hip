@@ -117,7 +117,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
         if ((rc = grow(&S.desc, &S.desc_cap, max_nseg * max_frames, "hipMalloc(host slot desc)"))) return rc;
         if ((rc = grow(&S.res, &S.res_cap, max_nseg, "hipMalloc(host slot res)"))) return rc;
         const size_t wsb = ws_decode_workspace_bytes(max_span, (u32)max_nseg, max_frames);
-        if (wsb && (rc = grow(&S.ws, &S.ws_cap, wsb, "hipMalloc(host slot workspace)"))) return rc;
+        if (wsb && S.ws_cap < wsb) {
+            if ((rc = grow(&S.ws, &S.ws_cap, wsb, "hipMalloc(host slot workspace)"))) return rc;
+            if ((e = hipMemset(S.ws, 0, 16)) != hipSuccess) return ws_set_err("hipMemset(host slot workspace)", e);
+        }
     }
 #define WS_TRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = ws_set_err(what, e); goto drain; } } while (0)
     for (size_t gi = 0; gi < groups.size(); ++gi) {

@@ -14,7 +14,7 @@
 //   every 16 KiB piece whose first byte lies in this segment's ownership range
 //   [end of segment s-1, end of segment s) the first item that can touch it.
 //   A segment that starts before the previous one ends (or lies outside [lo, hi))
-//   clears the "ordered" flag.
+//   marks the batch unordered.
 // K2 ws_piece_unmask_kernel — one 256-thread block per piece, 4 chunks per lane:
 //   payload loads first, then (while they are in flight) the piece pointer and the
 //   items it leads to (64 per load, hopping to the next segment when the piece
@@ -52,15 +52,15 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
                                                                  WebsocketFrameDesc_t* __restrict__ desc,
                                                                  WebsocketSegResult_t* __restrict__ res,
                                                                  u32x4* __restrict__ items, u32* __restrict__ nwork,
-                                                                 u64* __restrict__ ptr, u32* __restrict__ ordered,
-                                                                 u64 pbase, u64 lo, u64 hi) {
+                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
+                                                                 u32 gen, u64 pbase, u64 lo, u64 hi) {
     const u32 s = blockIdx.x * PWALK_T + threadIdx.x;
     if (s >= nseg) return;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const u64 so = seg_off[s], sl = seg_len[s];
     const u64 prev_end = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
     // out of order, or outside the declared range: the gated walker decodes the batch instead
-    if (prev_end > so || so < lo || sl > hi - so) atomicAnd(ordered, 0u);
+    if (prev_end > so || so < lo || sl > hi - so) *gptr<u32>(disorder) = gen;
     const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
     const u64 ibase = (u64)s * max_frames;
     const u64 sorg = so + lead0;                                            // origin-relative segment start
@@ -101,6 +101,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
     }
     const u32 cnt = nf + extra;
     put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);                         // pieces starting in the tail
+    if (s == nseg - 1) put_ptrs(ptr, pbase, sorg + sl, hi + lead0, PIECE_NONE);      // after the last segment
     ws_store_res(res + s, off, nf, status);
     *gptr<u32>(nwork + s) = cnt;
 }
@@ -120,8 +121,8 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 WebsocketFrameDesc_t* __restrict__ desc,
                                                                 WebsocketSegResult_t* __restrict__ res,
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
-                                                                u64* __restrict__ ptr, u32* __restrict__ ordered,
-                                                                u64 pbase, u64 lo, u64 hi) {
+                                                                u64* __restrict__ ptr, u32* __restrict__ disorder,
+                                                                u32 gen, u64 pbase, u64 lo, u64 hi) {
     static_assert(G == 16 || G == 32 || G == 64, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const u64 so = seg_off[sc], sl = seg_len[sc];
     const u64 prev_end = sc ? seg_off[sc - 1] + seg_len[sc - 1] : 0;
-    if (active && gl == 0 && (prev_end > so || so < lo || sl > hi - so)) atomicAnd(ordered, 0u);
+    if (active && gl == 0 && (prev_end > so || so < lo || sl > hi - so)) *gptr<u32>(disorder) = gen;
     const u64 dbase = desc_base ? desc_base[sc] : (u64)sc * max_frames;
     const u64 ibase = (u64)sc * max_frames;
     const u64 sorg = so + lead0;
@@ -207,6 +208,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         if (gl == 0) {
             const u32 cnt = nf + extra;
             put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);         // pieces starting in the tail
+            if (s == nseg - 1) put_ptrs(ptr, pbase, sorg + sl, hi + lead0, PIECE_NONE);
             ws_store_res(res + s, off, nf, status);
             *gptr<u32>(nwork + s) = cnt;
         }
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
                                                                   u32 max_frames, const u32x4* __restrict__ items,
                                                                   const u32* __restrict__ nwork,
                                                                   const u64* __restrict__ ptr,
-                                                                  const u32* __restrict__ ordered, u64 pbase,
+                                                                  const u32* __restrict__ disorder, u32 gen, u64 pbase,
                                                                   u64 c_lo, u64 c_hi) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     const u64 r0 = wc0 << 4, r1 = r0 + RW;
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
         reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
-    const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ordered));
+    const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
     u32 m[PIECE_U][4];
     u32 cov[PIECE_U];
 #pragma unroll
@@ -311,7 +313,10 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     }
 }
 
-// ws layout: [ordered u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
+// ws layout: [disorder u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
+// No per-call reset: K1 writes every piece pointer, and marks an unordered batch by
+// storing this call's generation number `gen` (never 0) into `disorder`, which the
+// workspace owner zeroes once when it allocates the workspace.
 static u64 piece_count(u64 lo_org, u64 hi_org) {
     return hi_org > lo_org ? ((hi_org - 1) >> PIECE_SHIFT) - (lo_org >> PIECE_SHIFT) + 1 : 0;
 }
@@ -323,47 +328,46 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     return b + (size_t)nseg * max_frames * 16 + 16;
 }
 
-// Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *ordered_out = the flag a gated
-// fallback walker must test.
+// Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *disorder_out = the word a gated
+// fallback walker compares with `gen`.
 int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3: 64/32/16 lanes per segment
 
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, const u32** ordered_out) {
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     const u64 npieces = piece_count(lo_org, hi_org);
     const u64 pbase = lo_org >> PIECE_SHIFT;
     const u64 c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
-    u32* ordered = reinterpret_cast<u32*>(ws);
+    u32* disorder = reinterpret_cast<u32*>(ws);
     u64* ptr = reinterpret_cast<u64*>(ws + 16);
     size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
     u32* nwork = reinterpret_cast<u32*>(ws + b);
     b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
     u32x4* items = reinterpret_cast<u32x4*>(ws + b);
-    hipError_t e = hipMemsetAsync(ws, 0xFF, 16 + npieces * 8, L.stream);    // ordered = ~0, ptr = PIECE_NONE
-    if (e != hipSuccess) return ws_set_err("hipMemsetAsync(piece workspace)", e);
+    hipError_t e;
     if (ws_piece_scan >= 1 && ws_piece_scan <= 3) {
         const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : 16);
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
         auto k = G == 64 ? ws_piece_scan_kernel<64> : (G == 32 ? ws_piece_scan_kernel<32> : ws_piece_scan_kernel<16>);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                           L.max_frames, L.desc_base, L.desc, L.res, items, nwork, ptr, ordered, pbase, lo, hi);
+                           L.max_frames, L.desc_base, L.desc, L.res, items, nwork, ptr, disorder, gen, pbase, lo, hi);
     }
     else
         hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, items, nwork,
-                           ptr, ordered, pbase, lo, hi);
+                           ptr, disorder, gen, pbase, lo, hi);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_walk_kernel launch", e);
     if (npieces) {
         if (nt == 1)
             hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, ordered, pbase, c_lo,
+                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, disorder, gen, pbase, c_lo,
                                c_hi);
         else
             hipLaunchKernelGGL((ws_piece_unmask_kernel<0>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, ordered, pbase, c_lo,
+                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, disorder, gen, pbase, c_lo,
                                c_hi);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
     }
-    *ordered_out = ordered;
+    *disorder_out = disorder;
     return 0;
 }

@@ -70,9 +70,9 @@ template <int U, int NT, bool DYN>
 __global__ __launch_bounds__(WALK_BLOCK) void ws_walker_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
-    WebsocketSegResult_t* __restrict__ res, u32* __restrict__ ctr, const u32* __restrict__ gate) {
+    WebsocketSegResult_t* __restrict__ res, u32* __restrict__ ctr, const u32* __restrict__ gate, u32 gate_gen) {
     // gated fallback (ws_piece.hip): run only if the piece path found the segments unordered
-    if (gate && *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(gate))) return;
+    if (gate && *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(gate)) != gate_gen) return;
     const u32 lane = threadIdx.x & 63;
     const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u32 nwaves = gridDim.x * WALK_WAVES;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(WALK_BLOCK) void ws_walker_kernel(
 }
 
 typedef void (*walker_t)(unsigned char*, const u64*, const u64*, u32, u32, const u64*, WebsocketFrameDesc_t*,
-                         WebsocketSegResult_t*, u32*, const u32*);
+                         WebsocketSegResult_t*, u32*, const u32*, u32);
 
 template <int U>
 static walker_t pick(int nt, int dyn) {
@@ -123,7 +123,8 @@ static walker_t pick(int nt, int dyn) {
     return nt == 1 ? ws_walker_kernel<U, 1, false> : (nt == 2 ? ws_walker_kernel<U, 2, false> : ws_walker_kernel<U, 0, false>);
 }
 
-int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr, const u32* gate) {
+int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr, const u32* gate,
+                     u32 gate_gen) {
     walker_t k = unroll == 8 ? pick<8>(nt, dyn) : (unroll == 2 ? pick<2>(nt, dyn) : pick<4>(nt, dyn));
     int per_cu = blocks_per_cu;
     if (per_cu <= 0) {
@@ -139,7 +140,7 @@ int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_
     hipError_t e;
     if (dyn && (e = hipMemsetAsync(ctr, 0, 16, L.stream)) != hipSuccess) return ws_set_err("hipMemsetAsync(counter)", e);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(WALK_BLOCK), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                       L.max_frames, L.desc_base, L.desc, L.res, ctr, gate);
+                       L.max_frames, L.desc_base, L.desc, L.res, ctr, gate, gate_gen);
     e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_walker_kernel launch", e);
 }
