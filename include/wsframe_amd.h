@@ -157,6 +157,32 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * Returns 0, or -1 for an unknown name. Not thread-safe against concurrent calls. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
+/* ---- Part 2c: batch encode + client masking -------------- */
+
+/* One frame to emit. The header is exactly websocketframeEncode's
+ * (websocketframe.c:167-202); with `masked` set the MASK bit and the 4 key bytes
+ * follow it (RFC 6455 §5.2-5.3, client-to-server frames — the reference's encoder
+ * never masks) and the payload is XORed with the key. 24 bytes, 8-B aligned. */
+typedef struct WebsocketEncodeDesc_t {
+    unsigned long long src_off;   /* payload offset in d_src */
+    unsigned long long len;       /* payload length (datalen) */
+    unsigned int mask_key;        /* key bytes in wire order: byte i = (mask_key >> 8*i) & 0xFF */
+    unsigned char type;           /* opcode (websocketframeEncode's type) */
+    unsigned char is_fin;         /* websocketframeEncode's is_fin */
+    unsigned char prev_is_fin;    /* websocketframeEncode's prev_is_fin */
+    unsigned char masked;         /* 1: client frame (MASK + key + XORed payload) */
+} WebsocketEncodeDesc_t;
+
+/* Encode nframes frames back to back into d_dst, asynchronously on hip_stream.
+ * d_wire_off (device, nframes + 1 u64) receives each frame's wire offset and, last,
+ * the total wire length. Bytes past dst_capacity are never written: size d_dst
+ * with Σ (len + 14) or read d_wire_off[nframes] first. d_src and d_dst must not
+ * overlap. Returns 0 or a negative launch error. */
+WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,
+                                                       const WebsocketEncodeDesc_t* d_frames, unsigned int nframes,
+                                                       unsigned char* d_dst, unsigned long long dst_capacity,
+                                                       unsigned long long* d_wire_off, void* hip_stream);
+
 /* ---- Part 3: synthetic batches (bench / test input only, not the decode path) - */
 
 /* Fill d_buf with nframes masked frames generated by util_amd/csrc/ws_synth.h.

@@ -54,3 +54,29 @@ def used_descs(desc, res, max_frames, desc_base=None):
         b = int(desc_base[s]) if desc_base is not None else s * max_frames
         out.append(desc[b:b + int(res[s]["n_frames"])])
     return np.concatenate(out) if out else desc[:0]
+
+
+def oracle_encode_frames(src, frames):
+    """Reference composition of a batch encode: websocketframeEncode's header (the
+    oracle restatement, pinned to the reference's golden vectors), then for masked
+    (client) frames the MASK bit, the 4 key bytes and the payload XORed with the key
+    (RFC 6455 §5.2-5.3). Returns (wire bytes, wire offsets incl. the total)."""
+    lib = load_oracle()
+    out = bytearray()
+    offs = []
+    for f in frames:
+        offs.append(len(out))
+        n = int(f["len"])
+        hl = lib.ws_oracle_encode_headlen(n)
+        h = (C.c_ubyte * 10)()
+        lib.ws_oracle_encode(h, int(f["is_fin"]), int(f["prev_is_fin"]), int(f["type"]), n)
+        hb = bytearray(bytes(h)[:hl])
+        body = np.frombuffer(bytes(src[int(f["src_off"]):int(f["src_off"]) + n]), dtype=np.uint8).copy()
+        if f["masked"]:
+            hb[1] |= 0x80
+            key = int(f["mask_key"]).to_bytes(4, "little")
+            hb += key
+            body ^= np.resize(np.frombuffer(key, dtype=np.uint8), n)
+        out += hb + body.tobytes()
+    offs.append(len(out))
+    return bytes(out), np.array(offs, dtype=np.uint64)

@@ -129,3 +129,31 @@ def test_reference_build_agrees_if_present():
             dv = None if d.value in (None, 1) else d.value - C.addressof(buf)
             outs.append((r, dv, dl.value, f.value, t.value, bytes(buf)))
         assert outs[0] == outs[1], i
+
+
+def test_oracle_encode_composition_roundtrip():
+    """the encode composition used as the batch-encode checker: its masked frames decode
+    (oracle a5 loop) back to the source payloads with websocketframeEncode's header fields"""
+    import wsynth  # noqa: F401  (tests/ on sys.path)
+    from oracle_lib import oracle_encode_frames, oracle_segments
+    from util_amd.wsframe import ENC_DTYPE
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 5, 125, 126, 127, 1000, 65535, 65536, 70000, 3]
+    src = rng.integers(0, 256, sum(lens) + 7, dtype=np.uint8)
+    fr = np.zeros(len(lens), ENC_DTYPE)
+    o = 7
+    for i, n in enumerate(lens):
+        fr[i] = (o, n, int(rng.integers(0, 2**32)), i % 3, i % 2, (i + 1) % 2, 1 if i % 4 else 0)
+        o += n
+    wire, offs = oracle_encode_frames(src, fr)
+    buf = np.frombuffer(wire, dtype=np.uint8).copy()
+    desc, res = oracle_segments(buf, [0], [len(buf)], len(lens))
+    assert int(res[0]["n_frames"]) == len(lens) and int(res[0]["consumed"]) == len(buf)
+    for i, n in enumerate(lens):
+        d = desc[i]
+        assert int(d["frame_off"]) == int(offs[i]) and int(d["datalen"]) == n
+        assert int(d["masked"]) == int(fr[i]["masked"]) and int(d["is_fin"]) == int(fr[i]["is_fin"])
+        assert int(d["type"]) == (int(fr[i]["type"]) if fr[i]["prev_is_fin"] else 0)
+        if n:
+            got = buf[int(d["data_off"]):int(d["data_off"]) + n]
+            assert np.array_equal(got, src[int(fr[i]["src_off"]):int(fr[i]["src_off"]) + n])

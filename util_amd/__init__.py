@@ -9,10 +9,10 @@ from ._lib import LIB_PATH, load_lib, build_lib  # noqa: F401
 from .wsframe import (  # noqa: F401
     WEBSOCKET_CONTINUE_FRAME, WEBSOCKET_TEXT_FRAME, WEBSOCKET_BINARY_FRAME, WEBSOCKET_CLOSE_FRAME,
     WEBSOCKET_PING_FRAME, WEBSOCKET_PONG_FRAME, WEBSOCKET_MAX_ENCODE_HEADLENGTH,
-    DESC_DTYPE, SEGRES_DTYPE, DATA_OFF_NULL,
+    DESC_DTYPE, SEGRES_DTYPE, ENC_DTYPE, DATA_OFF_NULL,
     SEG_OK, SEG_MAX_FRAMES, SEG_ERR_DECODE, SEG_ERR_LEN_WRAP,
     websocketframeDecode, websocketframeEncodeHeadLength, websocketframeEncode,
     websocketframeComputeSecAccept, websocketframeDecodeHandshakeRequest,
     websocketframeEncodeHandshakeResponse, websocketframeEncodeHandshakeResponseWithProtocol,
-    batch_decode_device, batch_decode_host, synth_device, synth_verify_device,
+    batch_decode_device, batch_decode_host, batch_encode_device, synth_device, synth_verify_device,
 )

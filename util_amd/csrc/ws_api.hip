@@ -76,6 +76,8 @@ struct WsDevState {
     unsigned slot = 0;
     u32* ws = nullptr;
     size_t ws_bytes = 0;
+    void* ews = nullptr;     // encode workspace (scan temp + piece pointers)
+    size_t ews_bytes = 0;
 };
 static WsDevState g_dev[WS_MAX_DEV];
 
@@ -110,6 +112,27 @@ static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream) {
     if ((e = hipMalloc(&ds->ws, sz)) != hipSuccess) return ws_set_err("hipMalloc(workspace)", e);
     if ((e = hipMemset(ds->ws, 0, 16)) != hipSuccess) return ws_set_err("hipMemset(workspace)", e);
     ds->ws_bytes = sz;
+    return 0;
+}
+
+// encode workspace (ws_encode.hip), same growth rules as the decode workspace
+int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
+    WsDevState* ds = nullptr;
+    int rc = dev_state(&ds);
+    if (rc) return rc;
+    hipError_t e;
+    if (ds->ews_bytes < bytes) {
+        if (ds->ews) {
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+            (void)hipFree(ds->ews);
+            ds->ews = nullptr;
+            ds->ews_bytes = 0;
+        }
+        const size_t sz = bytes + bytes / 4 + 4096;
+        if ((e = hipMalloc(&ds->ews, sz)) != hipSuccess) return ws_set_err("hipMalloc(encode workspace)", e);
+        ds->ews_bytes = sz;
+    }
+    *out = ds->ews;
     return 0;
 }
 

@@ -1,0 +1,230 @@
+// ws_encode.hip — batch frame encode + client-side masking.
+//
+// For every frame descriptor: the header websocketframeEncode writes
+// (websocketframe.c:167-202: first byte from (prev_is_fin, is_fin, type), 7/16/64-bit
+// length), plus — when `masked` — the MASK bit and the 4-byte key (RFC 6455 §5.3,
+// which the reference's encoder never sets), followed by the payload XORed with the
+// key. Frames are laid out back to back in d_dst.
+//
+// E1 hipcub exclusive scan of the wire lengths -> d_wire_off[0..n] (n+1: total last).
+// E2 one thread per frame: every 16 KiB output piece whose first byte lies in the
+//    frame's wire range gets the frame index (pieces past the end: none).
+// E3 one-shot 256-thread block per output piece, 4 x 16 B chunks per lane: the wave
+//    reads up to 64 frame records from its piece's first frame, then every chunk that
+//    lies inside one payload is one unaligned 16-B source load + XOR + aligned store;
+//    chunks that straddle headers or frame edges are assembled byte by byte (header
+//    bytes computed, payload bytes loaded). The output is dense, so every chunk but
+//    the batch's first and last is written with one 16-B store, exactly once.
+#include <hipcub/hipcub.hpp>
+
+#include "ws_common.h"
+
+#define ENC_T 256
+#define ENC_U 4
+#define ENC_SHIFT 14
+#define ENC_NONE 0xFFFFFFFFu
+
+__device__ __forceinline__ u32 enc_hl(u64 len) { return len < 126 ? 2u : (len <= 0xFFFFull ? 4u : 10u); }
+
+struct EncFrame {
+    u64 src, len, off;   // payload source offset, payload length, wire offset (dst-relative)
+    u32 key, hl;         // key (LE), header bytes incl. mask key
+    u32 b0, masked;
+};
+
+__device__ __forceinline__ EncFrame enc_load(const WebsocketEncodeDesc_t* f, const u64* wire_off, u32 i) {
+    const gu32x4* q = gptr<u32x4>(f + i);
+    const u32x4 a = q[0];
+    const u32 w4 = gptr<u32>(f + i)[4], w5 = gptr<u32>(f + i)[5];
+    EncFrame e;
+    e.src = (u64)a.x | ((u64)a.y << 32);
+    e.len = (u64)a.z | ((u64)a.w << 32);
+    e.key = w4;
+    const u32 type = w5 & 0xFFu, fin = (w5 >> 8) & 0xFFu, prev_fin = (w5 >> 16) & 0xFFu;
+    e.masked = (w5 >> 24) != 0;
+    const u32 op = prev_fin ? type : 0u;                                     // websocketframe.c:176-202
+    e.b0 = (fin ? (op | 0x80u) : op) & 0xFFu;
+    e.hl = enc_hl(e.len) + (e.masked ? 4u : 0u);
+    e.off = wire_off[i];
+    return e;
+}
+
+// byte j of the frame's header (j < hl)
+__device__ __forceinline__ u32 enc_header_byte(const EncFrame& e, u32 j) {
+    const u32 n = enc_hl(e.len);
+    if (j == 0) return e.b0;
+    if (j == 1) return (n == 2 ? (u32)e.len : (n == 4 ? 126u : 127u)) | (e.masked ? 0x80u : 0u);
+    if (j < n) return (u32)(e.len >> (8 * (n - 1 - j))) & 0xFFu;            // big-endian extended length
+    return (e.key >> (8 * (j - n))) & 0xFFu;                                 // mask key, wire order
+}
+
+struct WireLen {
+    const WebsocketEncodeDesc_t* f;
+    u32 n;
+    __host__ __device__ u64 operator()(u32 i) const {
+        if (i >= n) return 0;
+        const u64 len = f[i].len;
+        return (u64)(len < 126 ? 2u : (len <= 0xFFFFull ? 4u : 10u)) + (f[i].masked ? 4u : 0u) + len;
+    }
+};
+
+__global__ __launch_bounds__(256) void ws_enc_ptr_kernel(const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                         const u64* __restrict__ wire_off, u32* __restrict__ ptr,
+                                                         u64 lead0, u64 npieces) {
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i > n) return;
+    const u64 a = i ? wire_off[i] + lead0 : 0;                               // frame 0 also owns the origin
+    const u64 b = i < n ? wire_off[i + 1] + lead0 : ((npieces) << ENC_SHIFT);
+    const u32 val = i < n ? i : ENC_NONE;                                    // i == n: pieces past the end
+    for (u64 p = (a + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT; (p << ENC_SHIFT) < b && p < npieces; ++p) ptr[p] = val;
+}
+
+__device__ __forceinline__ void put_byte(u32x4& w, u32 b, u32 v) {
+    const u32 sh = 8u * (b & 3);
+    w.x |= b < 4 ? v << sh : 0u;
+    w.y |= (b >> 2) == 1 ? v << sh : 0u;
+    w.z |= (b >> 2) == 2 ? v << sh : 0u;
+    w.w |= b >= 12 ? v << sh : 0u;
+}
+
+typedef u32x4 __attribute__((aligned(1))) u32x4u;
+
+template <int NT>
+__global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char* __restrict__ src,
+                                                            const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                            const u64* __restrict__ wire_off,
+                                                            const u32* __restrict__ ptr, unsigned char* __restrict__ dst,
+                                                            u64 capacity) {
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
+    const u64 total = min(wire_off[n], capacity);                            // never write past the capacity
+    const u64 r0 = (((u64)blockIdx.x << ENC_SHIFT) + (u64)wv * (64 * ENC_U * 16));  // origin-relative
+    const u64 r1 = r0 + 64 * ENC_U * 16;
+    const u32 first = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
+    if (first == ENC_NONE) return;
+    // chunk state: fast = one payload source for the whole chunk
+    u64 fsrc[ENC_U];
+    u32 fkey[ENC_U];
+    u32 kind[ENC_U];                                                          // 0 untouched, 1 fast, 2 assembled
+    u32x4 w[ENC_U];
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) { kind[u] = 0; fsrc[u] = 0; fkey[u] = 0; w[u] = (u32x4){0, 0, 0, 0}; }
+    for (u32 k = first; k < n;) {
+        const u32 j = k + lane;
+        const bool valid = j < n;
+        EncFrame e = {};
+        if (valid) e = enc_load(f, wire_off, j);
+        const u64 eo = e.off + lead0, ee = eo + e.hl + e.len;                // origin-relative extent
+        const u64 past = __ballot(valid && eo >= r1);
+        const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
+        u64 hm = __ballot(valid && lane < nlim && ee > r0);
+        while (hm) {
+            const int i = __builtin_ctzll(hm);
+            hm &= hm - 1;
+            EncFrame g;
+            g.src = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)e.src, i)) |
+                    ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(e.src >> 32), i) << 32);
+            g.len = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)e.len, i)) |
+                    ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(e.len >> 32), i) << 32);
+            g.off = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)eo, i)) |
+                    ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(eo >> 32), i) << 32);   // origin-relative
+            g.key = (u32)__builtin_amdgcn_readlane((int)e.key, i);
+            g.hl = (u32)__builtin_amdgcn_readlane((int)e.hl, i);
+            g.b0 = (u32)__builtin_amdgcn_readlane((int)e.b0, i);
+            g.masked = (u32)__builtin_amdgcn_readlane((int)e.masked, i);
+            const u64 d0 = g.off + g.hl, d1 = d0 + g.len;                    // payload (origin-relative)
+            const u32 rk = g.masked ? rotl32(g.key, 8u * (u32)(d0 & 3)) : 0u;  // key phase of aligned chunks
+#pragma unroll
+            for (int u = 0; u < ENC_U; ++u) {
+                const u64 x = r0 + (u64)(u * 1024 + lane * 16);
+                if (x + 16 <= g.off || x >= d1) continue;                    // no byte of this frame
+                if (x >= d0 && x + 16 <= d1) {                               // inside the payload
+                    kind[u] = 1;
+                    fsrc[u] = g.src + (x - d0);
+                    fkey[u] = rk;
+                    continue;
+                }
+                kind[u] = 2;                                                 // header / edge bytes
+                const u32 lo = g.off > x ? (u32)(g.off - x) : 0u, hi = d1 < x + 16 ? (u32)(d1 - x) : 16u;
+                for (u32 b = lo; b < hi; ++b) {
+                    const u64 y = x + b - g.off;                             // byte index in the frame
+                    u32 v;
+                    if (y < g.hl) {
+                        v = enc_header_byte(g, (u32)y);
+                    } else {
+                        const u64 pi = y - g.hl;
+                        v = *reinterpret_cast<const gu8*>(reinterpret_cast<uintptr_t>(src + g.src + pi));
+                        if (g.masked) v ^= (g.key >> (8 * (u32)(pi & 3))) & 0xFFu;
+                    }
+                    put_byte(w[u], b, v);
+                }
+            }
+        }
+        if (nlim < 64) break;
+        k += 64;
+    }
+    // payload-interior chunks: one unaligned 16-B source load each (issued together)
+    u32x4 v[ENC_U];
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) {
+        v[u] = (u32x4){0, 0, 0, 0};
+        if (kind[u] == 1) v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + fsrc[u]));
+    }
+    const u64 out_lo = lead0, out_hi = lead0 + total;                        // origin-relative output bytes
+#pragma unroll
+    for (int u = 0; u < ENC_U; ++u) {
+        if (!kind[u]) continue;
+        const u64 x = r0 + (u64)(u * 1024 + lane * 16);
+        const u32x4 o = kind[u] == 1 ? (v[u] ^ fkey[u]) : w[u];
+        gu32x4* const pc = base + (x >> 4);
+        if (x >= out_lo && x + 16 <= out_hi) {
+            st16<NT>(o, pc);
+        } else {                                                             // batch start / end
+            gu8* const pb = reinterpret_cast<gu8*>(pc);
+            for (u32 q = 0; q < 16; ++q) {
+                if (x + q < out_lo || x + q >= out_hi) continue;
+                const u32 wq = q < 4 ? o.x : (q < 8 ? o.y : (q < 12 ? o.z : o.w));
+                pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
+            }
+        }
+    }
+}
+
+int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out);
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,
+                                                                  const WebsocketEncodeDesc_t* d_frames,
+                                                                  unsigned int nframes, unsigned char* d_dst,
+                                                                  unsigned long long dst_capacity,
+                                                                  unsigned long long* d_wire_off, void* hip_stream) {
+    if (nframes == 0) return 0;
+    if (!d_src || !d_frames || !d_dst || !d_wire_off) return ws_set_msg("websocketframeBatchEncodeDevice: invalid argument");
+    if (reinterpret_cast<uintptr_t>(d_frames) & 7) return ws_set_msg("websocketframeBatchEncodeDevice: d_frames not 8-B aligned");
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    const u64 lead0 = reinterpret_cast<uintptr_t>(d_dst) & 15;
+    const u64 npieces = (dst_capacity + lead0 + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT;
+    WireLen op{d_frames, nframes};
+    hipcub::CountingInputIterator<u32> cnt(0);
+    hipcub::TransformInputIterator<u64, WireLen, hipcub::CountingInputIterator<u32>> in(cnt, op);
+    size_t scan_bytes = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, d_wire_off, nframes + 1, st);
+    if (e != hipSuccess) return ws_set_err("hipcub scan (size)", e);
+    const size_t ptr_off = (scan_bytes + 255) & ~(size_t)255;
+    void* ws = nullptr;
+    int rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws);
+    if (rc) return rc;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
+        return ws_set_err("hipcub scan", e);
+    u32* ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
+    hipLaunchKernelGGL(ws_enc_ptr_kernel, dim3((nframes + 1 + 255) / 256), dim3(256), 0, st, d_frames, nframes,
+                       d_wire_off, ptr, lead0, npieces);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
+    if (npieces) {
+        hipLaunchKernelGGL((ws_enc_copy_kernel<1>), dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
+                           d_wire_off, ptr, d_dst, (u64)dst_capacity);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
+    }
+    return 0;
+}

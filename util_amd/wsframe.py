@@ -27,6 +27,9 @@ BATCH_PAD = 32  # WEBSOCKET_BATCH_PAD: readable device bytes required after ever
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("data_off", "<u8"), ("datalen", "<u8"), ("ret", "<i4"),
                        ("is_fin", "u1"), ("type", "u1"), ("masked", "u1"), ("hdrlen", "u1")])
 SEGRES_DTYPE = np.dtype([("consumed", "<u8"), ("n_frames", "<u4"), ("status", "<i4")])
+ENC_DTYPE = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("mask_key", "<u4"), ("type", "u1"), ("is_fin", "u1"),
+                      ("prev_is_fin", "u1"), ("masked", "u1")])
+assert ENC_DTYPE.itemsize == 24
 assert DESC_DTYPE.itemsize == C.sizeof(WsDesc) == 32
 assert SEGRES_DTYPE.itemsize == C.sizeof(WsSegRes) == 16
 
@@ -136,6 +139,18 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
                                                     nseg, max_frames, _ptr(desc_base), _ptr(desc), _ptr(res),
                                                     _stream(stream))
     check(rc, "websocketframeBatchDecodeDevice")
+
+
+def batch_encode_device(src, frames, dst, wire_off, capacity=None, stream=None):
+    """websocketframeBatchEncodeDevice on torch CUDA tensors: src (uint8 payload bytes),
+    frames (uint8 tensor holding ENC_DTYPE records), dst (uint8), wire_off (int64,
+    nframes + 1); async on `stream`. capacity defaults to dst.numel()."""
+    n = frames.numel() // ENC_DTYPE.itemsize
+    assert wire_off.numel() >= n + 1
+    cap = dst.numel() if capacity is None else capacity
+    rc = load_lib().websocketframeBatchEncodeDevice(_ptr(src), _ptr(frames), n, _ptr(dst), cap, _ptr(wire_off),
+                                                    _stream(stream))
+    check(rc, "websocketframeBatchEncodeDevice")
 
 
 def batch_decode_host(buf, seg_off, seg_len, max_frames, device=0):
