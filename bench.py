@@ -159,6 +159,104 @@ class Workload:
         self.torch.cuda.empty_cache()
 
 
+class EncodeWorkload:
+    """Client-side encode of the same frames: plaintext payloads resident
+    in HBM -> masked wire frames (websocketframeEncode headers + MASK + key + XOR)."""
+
+    def __init__(self, name, dev, seed_offset=0):
+        import torch
+        from util_amd import wsframe as W
+        n, pk, fl, bk, seed, fps = Workload.CONFIGS[name]
+        assert pk == 0, "encode bench: fixed-size configs only"
+        self.torch, self.W, self.dev, self.name, self.fps = torch, W, dev, name, fps
+        self.nframes, self.plen = n, fl
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + seed_offset)
+        self.src = torch.randint(0, 256, (n * fl,), dtype=torch.uint8, device=dev, generator=g)
+        fr = np.zeros(n, W.ENC_DTYPE)
+        fr["src_off"] = np.arange(n, dtype=np.uint64) * fl
+        fr["len"] = fl
+        fr["mask_key"] = np.random.default_rng(seed).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        fr["type"], fr["is_fin"], fr["prev_is_fin"], fr["masked"] = 2, 1, 1, 1
+        self.frames = torch.from_numpy(fr.view(np.uint8)).to(dev)
+        self.hl = (2 if fl < 126 else (4 if fl <= 0xFFFF else 10)) + 4
+        self.wire_bytes = n * (fl + self.hl)
+        self.payload_bytes = n * fl
+        self.dst = torch.empty(self.wire_bytes + 256, dtype=torch.uint8, device=dev)
+        self.off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    @property
+    def algo_bytes(self):                  # read every payload byte, write every wire byte
+        return self.payload_bytes + self.wire_bytes
+
+    def step(self):
+        self.W.batch_encode_device(self.src, self.frames, self.dst, self.off, capacity=self.wire_bytes)
+
+    def verify(self):
+        """decode the encoded wire on the device (rx segments of fps frames) and compare with the source"""
+        t = self.torch
+        n, fps = self.nframes, self.fps
+        fl = self.wire_bytes // n
+        so = t.arange(0, n, fps, device=self.dev, dtype=t.int64) * fl
+        sl = t.full_like(so, fps * fl)
+        desc = t.empty(len(so) * fps * 32, dtype=t.uint8, device=self.dev)
+        res = t.empty(len(so) * 16, dtype=t.uint8, device=self.dev)
+        ok = int(self.off[-1].item()) == self.wire_bytes
+        self.W.batch_decode_device(self.dst, so, sl, fps, desc, res)
+        body = self.dst[:self.wire_bytes].view(n, fl)[:, self.hl:]
+        ok = ok and t.equal(body, self.src.view(n, self.plen))
+        return 0 if ok else 1
+
+
+def run_encode(args, dev, world, rank):
+    import torch
+    from util_amd import dist as D
+    wl = EncodeWorkload(args.config, dev, seed_offset=rank)
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        wl.step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = D.allreduce([time.perf_counter() - t0], op="max", device=dev)[0]
+    kern_ms = np.array([a.elapsed_time(b) for a, b in zip(starts, ends)])
+    mism = int(D.allreduce([wl.verify()], device=dev)[0])
+    mean_kern = float(kern_ms.mean()) / 1e3
+    achieved = wl.algo_bytes / mean_kern / 1e9
+    out = {
+        "metric": "WebSocket client encode+mask GiB/s (device-resident), %d x %d B frames" % (wl.nframes, wl.plen),
+        "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint payloads in HBM)",
+        "config": {"workload": "encode " + Workload.DESCRIPTION[args.config], "config": args.config,
+                   "frames_per_gpu": wl.nframes, "wire_bytes_per_gpu": wl.wire_bytes,
+                   "payload_bytes_per_gpu": wl.payload_bytes},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "kernel": "ws_enc_copy_kernel", "algo_bytes_per_launch": wl.algo_bytes,
+                     "timed": "HIP events around each encode call: hipcub scan + ws_enc_ptr_kernel + "
+                              "ws_enc_copy_kernel",
+                     "kernel_ms_mean": round(mean_kern * 1e3, 4)},
+        "verified": mism == 0,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    return mism
+
+
 def end_to_end(wl, runs=2):
     """websocketframeBatchDecodeHost on a pinned host copy of the whole batch: H2D + decode + D2H,
     pipelined over ~64 MiB segment groups on 3 streams (SURVEY §8d end-to-end). Reported beside
@@ -259,6 +357,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
+    ap.add_argument("--op", default="decode", choices=["decode", "encode"],
+                    help="decode (the headline) or client-side encode + mask of the same frames")
     args = ap.parse_args()
     from util_amd import wsframe as W
     path = DEFAULT_PATH if args.path is None else args.path
@@ -275,6 +375,11 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.op == "encode":
+        mism = run_encode(args, dev, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(1 if mism else 0)
 
     wl = Workload.make(args.config, dev, seed_offset=rank)
     torch.cuda.synchronize()

@@ -90,9 +90,12 @@ enum {
     WEBSOCKET_SEG_MAX_FRAMES = 1,      /* descriptor capacity reached; resubmit from `consumed` */
     WEBSOCKET_SEG_ERR_DECODE = -1,     /* a frame returned ret < 0 (int truncation, websocketframe.c:164):
                                           the reactor marks the channel invalid (net_reactor.c:518-520) */
-    WEBSOCKET_SEG_ERR_LEN_WRAP = -2    /* masked frame whose u64 length sum wraps (websocketframe.c:149):
+    WEBSOCKET_SEG_ERR_LEN_WRAP = -2,   /* masked frame whose u64 length sum wraps (websocketframe.c:149):
                                           the reference would unmask past the buffer (undefined behaviour);
                                           fenced off here, nothing is written for that frame */
+    WEBSOCKET_SEG_ERR_OUT_SPACE = -3   /* reassembly only: the bodies outgrow the segment's output region
+                                          (possible only through the (int) return truncation of frames
+                                          >= 2 GiB, websocketframe.c:164) */
 };
 
 /* Per-segment result. 16 bytes. */
@@ -156,6 +159,37 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * loads+stores / 2 nontemporal stores), "blocks_per_cu" (0 = resident limit).
  * Returns 0, or -1 for an unknown name. Not thread-safe against concurrent calls. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
+
+/* ---- Part 2b: fused decode + fragmented-message reassembly -- */
+
+/* One reassembled message body in the output buffer. 32 bytes. */
+typedef struct WebsocketMsgDesc_t {
+    unsigned long long out_off;   /* body offset from d_out */
+    unsigned long long len;       /* body length = sum of its frames' datalen in this batch */
+    unsigned int first_frame;     /* its first frame's index among the segment's descriptors */
+    unsigned int n_frames;        /* its frames in this batch */
+    unsigned int complete;        /* 1: closed by a FIN frame (delivered); 0: still open at the segment end */
+    unsigned int continued;       /* 1: continues a message left open by an earlier batch (d_open) */
+} WebsocketMsgDesc_t;
+
+/* Decode every segment exactly as websocketframeBatchDecodeDevice (same descriptors and
+ * results; slots s*max_frames), then deliver messages as the reactor's stream hook does
+ * with websocket glue: the unmasked body of every consumed frame joins
+ * the connection's pending message, and a FIN frame closes it — the message body is the
+ * concatenation of its frames' bodies (a FIN frame with nothing pending is one message).
+ * Bodies are gathered, unmasked, back to back from d_out + (d_out_off ? d_out_off[s]
+ * : d_seg_off[s]) (room for seg_len[s] bytes each); the wire buffer is only read. Message
+ * descriptors of segment s are d_msg[s*max_frames + i], i < d_nmsg[s]. d_open (optional,
+ * one byte per segment, in/out): 1 = a message is pending from the previous batch.
+ * Asynchronous on hip_stream; returns 0 or a negative launch error. */
+WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(const unsigned char* d_buf, unsigned long long buflen,
+                                                           const unsigned long long* d_seg_off,
+                                                           const unsigned long long* d_seg_len, unsigned int nseg,
+                                                           unsigned int max_frames, WebsocketFrameDesc_t* d_desc,
+                                                           WebsocketSegResult_t* d_res, unsigned char* d_out,
+                                                           const unsigned long long* d_out_off,
+                                                           WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
+                                                           unsigned char* d_open, void* hip_stream);
 
 /* ---- Part 2c: batch encode + client masking -------------- */
 

@@ -80,3 +80,43 @@ def oracle_encode_frames(src, frames):
         out += hb + body.tobytes()
     offs.append(len(out))
     return bytes(out), np.array(offs, dtype=np.uint64)
+
+
+def oracle_reassemble(wire, seg_off, seg_len, max_frames, open_in=None, out_off=None):
+    """Checker for websocketframeBatchReassembleDevice, composed from the decode oracle
+    (pinned to the reference's golden vectors): the a5 loop runs on a copy of the wire
+    (unmasking in place, as websocketframeDecode does), then the delivery rule of
+    SURVEY §8a row a6 is applied per segment — the bodies of consecutive consumed frames
+    form the pending message, a FIN frame closes it.
+    Returns (desc, res, msgs[s] = [(out_off, len, first, n, complete, continued)],
+    regions[s] = (out_off, expected body bytes), open_out)."""
+    buf = np.asarray(wire, dtype=np.uint8).copy()
+    desc, res = oracle_segments(buf, seg_off, seg_len, max_frames)
+    res = res.copy()
+    msgs, regions, open_out = [], [], []
+    for s in range(len(seg_off)):
+        ob = int(out_off[s]) if out_off is not None else int(seg_off[s])
+        opened = int(open_in[s]) if open_in is not None else 0
+        cont, first, q, q0 = opened, 0, 0, 0
+        bodies, ms = [], []
+        for k in range(int(res[s]["n_frames"])):
+            d = desc[s * max_frames + k]
+            if int(d["ret"]) <= 0:
+                break
+            n = int(d["datalen"])
+            if n > int(seg_len[s]) - q:
+                res[s]["status"] = -3
+                break
+            a = int(d["data_off"])
+            bodies.append(buf[a:a + n] if n else buf[:0])
+            q += n
+            opened = 1
+            if int(d["is_fin"]):
+                ms.append((ob + q0, q - q0, first, k + 1 - first, 1, cont))
+                first, q0, cont, opened = k + 1, q, 0, 0
+        if opened and len(bodies) > first:
+            ms.append((ob + q0, q - q0, first, len(bodies) - first, 0, cont))
+        msgs.append(ms)
+        regions.append((ob, np.concatenate(bodies) if bodies else np.zeros(0, np.uint8)))
+        open_out.append(opened)
+    return desc, res, msgs, regions, np.array(open_out, dtype=np.uint8)

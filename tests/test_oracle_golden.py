@@ -157,3 +157,22 @@ def test_oracle_encode_composition_roundtrip():
         if n:
             got = buf[int(d["data_off"]):int(d["data_off"]) + n]
             assert np.array_equal(got, src[int(fr[i]["src_off"]):int(fr[i]["src_off"]) + n])
+
+
+def test_oracle_reassemble_delivery_rule():
+    """the reassembly checker on a hand-built connection: [A no FIN][B FIN][C FIN][D no FIN]
+    -> messages A+B, C (complete) and D (pending); a carried-in open message marks the first
+    message `continued`; an error frame ends delivery"""
+    from oracle_lib import oracle_reassemble
+
+    def frame(b0, body, key=b"\x01\x02\x03\x04"):
+        masked = bytes(x ^ key[i % 4] for i, x in enumerate(body))
+        return bytes([b0, 0x80 | len(body)]) + key + masked
+    wire = frame(0x02, b"alpha") + frame(0x80, b"beta") + frame(0x81, b"gamma") + frame(0x00, b"delta")
+    w = np.frombuffer(wire, dtype=np.uint8)
+    desc, res, msgs, regions, op = oracle_reassemble(w, [0], [len(wire)], 8)
+    assert int(res[0]["n_frames"]) == 4 and int(res[0]["consumed"]) == len(wire)
+    assert [m[1:] for m in msgs[0]] == [(9, 0, 2, 1, 0), (5, 2, 1, 1, 0), (5, 3, 1, 0, 0)]
+    assert bytes(regions[0][1]) == b"alphabetagammadelta" and op[0] == 1
+    _, _, msgs2, _, op2 = oracle_reassemble(w, [0], [len(wire)], 8, open_in=[1])
+    assert msgs2[0][0][5] == 1 and msgs2[0][1][5] == 0

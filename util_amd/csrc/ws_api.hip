@@ -136,6 +136,24 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     return 0;
 }
 
+// per-call generation number for the piece path's disorder word (never 0)
+u32 ws_next_gen() {
+    static std::atomic<u32> s_gen{0};
+    u32 gen = ++s_gen;
+    if (gen == 0) gen = ++s_gen;                                       // 0 = a fresh workspace's value
+    return gen;
+}
+
+// the per-device decode workspace (first 16 bytes zeroed at allocation)
+int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
+    WsDevState* ds = nullptr;
+    int rc = dev_state(&ds);
+    if (rc) return rc;
+    if ((rc = workspace(ds, bytes, stream))) return rc;
+    *out = ds->ws;
+    return 0;
+}
+
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     const WsTuning t = g_tune;
     if (t.path == 3) return ws_piece_workspace_bytes(span, nseg, max_frames);
@@ -170,9 +188,7 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         ws = ds->ws;
     }
     if (t.path == 3) {
-        static std::atomic<u32> s_gen{0};
-        u32 gen = ++s_gen;
-        if (gen == 0) gen = ++s_gen;                                   // 0 = a fresh workspace's value
+        const u32 gen = ws_next_gen();
         const u32* disorder = nullptr;
         if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder))) return rc;
         // fallback for segments out of buffer order: a small gated walker grid (exits at once otherwise)

@@ -217,6 +217,16 @@ struct WsLaunch {
 int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr,
                      const u32* gate = nullptr, u32 gate_gen = 0);
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
+struct PieceWs {          // ws_piece.hip workspace views after K1
+    u32* disorder;
+    u64* ptr;
+    u32* nwork;           // items per segment (frames walked, incl. an unconsumed ret==0 frame)
+    u32x4* items;         // per descriptor slot s*max_frames+k: P0|rk_lo<<48, P1|rk_hi<<48 (origin-relative)
+    u64 npieces, pbase, c_lo, c_hi;
+};
+int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out);
+u32 ws_next_gen();
+int ws_device_workspace(size_t bytes, hipStream_t stream, void** out);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
 // (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes whose

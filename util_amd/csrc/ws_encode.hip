@@ -11,10 +11,10 @@
 //    frame's wire range gets the frame index (pieces past the end: none).
 // E3 one-shot 256-thread block per output piece, 4 x 16 B chunks per lane: the wave
 //    reads up to 64 frame records from its piece's first frame, then every chunk that
-//    lies inside one payload is one unaligned 16-B source load + XOR + aligned store;
-//    chunks that straddle headers or frame edges are assembled byte by byte (header
-//    bytes computed, payload bytes loaded). The output is dense, so every chunk but
-//    the batch's first and last is written with one 16-B store, exactly once.
+//    lies inside one payload is one unaligned 16-B source load + XOR + aligned store.
+// E4 one thread per frame assembles the other chunks whose first byte lies in its wire
+//    extent (header bytes, frame edges; header bytes computed, payload bytes loaded)
+//    and stores each with one 16-B store. Every output chunk is written exactly once.
 #include <hipcub/hipcub.hpp>
 
 #include "ws_common.h"
@@ -107,10 +107,9 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
     // chunk state: fast = one payload source for the whole chunk
     u64 fsrc[ENC_U];
     u32 fkey[ENC_U];
-    u32 kind[ENC_U];                                                          // 0 untouched, 1 fast, 2 assembled
-    u32x4 w[ENC_U];
+    u32 kind[ENC_U];                                                          // 1: inside one payload
 #pragma unroll
-    for (int u = 0; u < ENC_U; ++u) { kind[u] = 0; fsrc[u] = 0; fkey[u] = 0; w[u] = (u32x4){0, 0, 0, 0}; }
+    for (int u = 0; u < ENC_U; ++u) { kind[u] = 0; fsrc[u] = 0; fkey[u] = 0; }
     for (u32 k = first; k < n;) {
         const u32 j = k + lane;
         const bool valid = j < n;
@@ -146,20 +145,7 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
                     fkey[u] = rk;
                     continue;
                 }
-                kind[u] = 2;                                                 // header / edge bytes
-                const u32 lo = g.off > x ? (u32)(g.off - x) : 0u, hi = d1 < x + 16 ? (u32)(d1 - x) : 16u;
-                for (u32 b = lo; b < hi; ++b) {
-                    const u64 y = x + b - g.off;                             // byte index in the frame
-                    u32 v;
-                    if (y < g.hl) {
-                        v = enc_header_byte(g, (u32)y);
-                    } else {
-                        const u64 pi = y - g.hl;
-                        v = *reinterpret_cast<const gu8*>(reinterpret_cast<uintptr_t>(src + g.src + pi));
-                        if (g.masked) v ^= (g.key >> (8 * (u32)(pi & 3))) & 0xFFu;
-                    }
-                    put_byte(w[u], b, v);
-                }
+                // chunks with header bytes or a frame edge: ws_enc_edge_kernel
             }
         }
         if (nlim < 64) break;
@@ -172,20 +158,79 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
         v[u] = (u32x4){0, 0, 0, 0};
         if (kind[u] == 1) v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + fsrc[u]));
     }
-    const u64 out_lo = lead0, out_hi = lead0 + total;                        // origin-relative output bytes
+    const u64 out_hi = lead0 + total;                                        // origin-relative end
 #pragma unroll
     for (int u = 0; u < ENC_U; ++u) {
-        if (!kind[u]) continue;
         const u64 x = r0 + (u64)(u * 1024 + lane * 16);
-        const u32x4 o = kind[u] == 1 ? (v[u] ^ fkey[u]) : w[u];
-        gu32x4* const pc = base + (x >> 4);
-        if (x >= out_lo && x + 16 <= out_hi) {
-            st16<NT>(o, pc);
-        } else {                                                             // batch start / end
+        if (kind[u] == 1 && x + 16 <= out_hi) st16<NT>(v[u] ^ fkey[u], base + (x >> 4));
+    }
+}
+
+// Every 16-B output chunk that is not inside one payload (header bytes, frame edges,
+// the batch's first and last chunk): assembled by the frame whose wire extent holds the
+// chunk's first byte (frame 0 also takes a chunk starting before the output), byte by
+// byte — header bytes computed, payload bytes loaded — and stored once.
+__global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* __restrict__ src,
+                                                          const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                          const u64* __restrict__ wire_off,
+                                                          unsigned char* __restrict__ dst, u64 capacity) {
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
+    const u64 total = min(wire_off[n], capacity);
+    const u64 out_lo = lead0, out_hi = lead0 + total;
+    const EncFrame e = enc_load(f, wire_off, i);
+    const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
+    u64 X = i ? ((o + 15) & ~15ull) : (o & ~15ull);                           // first chunk start owned
+    const u64 lim = d1 < out_hi ? d1 : out_hi;                               // interior chunks end here
+    for (; X < d1 && X < out_hi; X += 16) {
+        if (X >= d0 && X + 16 <= lim) {                                      // payload interior: copy kernel
+            X = (lim - 16) & ~15ull;                                         // last interior chunk
+            continue;
+        }
+        u32x4 w = {0, 0, 0, 0};
+        u32 g = i;
+        EncFrame h = e;
+        for (;;) {
+            const u64 ho = h.off + lead0, hd0 = ho + h.hl, hd1 = hd0 + h.len;
+            const u64 lo = ho > X ? ho : X, hi = hd1 < X + 16 ? hd1 : X + 16;
+            // this frame's payload bytes in the chunk come from ONE 16-B window of the source
+            // (kept inside the payload: start = min(first index, len - 16)); byte loads only
+            // for payloads shorter than 16 B
+            const u64 pa = lo > hd0 ? lo - hd0 : 0;                          // first payload index needed
+            const u64 wst = h.len >= 16 ? (pa < h.len - 16 ? pa : h.len - 16) : 0;
+            u32x4 win = {0, 0, 0, 0};
+            if (h.len >= 16 && hi > hd0)
+                win = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + h.src + wst));
+            for (u64 y = lo; y < hi; ++y) {
+                u32 v;
+                if (y < hd0) {
+                    v = enc_header_byte(h, (u32)(y - ho));
+                } else {
+                    const u64 pi = y - hd0;
+                    if (h.len >= 16) {
+                        const u32 q = (u32)(pi - wst);
+                        const u32 wq = q < 4 ? win.x : (q < 8 ? win.y : (q < 12 ? win.z : win.w));
+                        v = (wq >> (8u * (q & 3))) & 0xFFu;
+                    } else {
+                        v = *reinterpret_cast<const gu8*>(reinterpret_cast<uintptr_t>(src + h.src + pi));
+                    }
+                    if (h.masked) v ^= (h.key >> (8 * (u32)(pi & 3))) & 0xFFu;
+                }
+                put_byte(w, (u32)(y - X), v);
+            }
+            if (hd1 >= X + 16 || ++g >= n) break;
+            h = enc_load(f, wire_off, g);
+        }
+        gu32x4* const pc = base + (X >> 4);
+        if (X >= out_lo && X + 16 <= out_hi) {
+            *pc = w;
+        } else {
             gu8* const pb = reinterpret_cast<gu8*>(pc);
             for (u32 q = 0; q < 16; ++q) {
-                if (x + q < out_lo || x + q >= out_hi) continue;
-                const u32 wq = q < 4 ? o.x : (q < 8 ? o.y : (q < 12 ? o.z : o.w));
+                if (X + q < out_lo || X + q >= out_hi) continue;
+                const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
                 pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
             }
         }
@@ -226,5 +271,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
                            d_wire_off, ptr, d_dst, (u64)dst_capacity);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
+    hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, d_src, d_frames, nframes,
+                       d_wire_off, d_dst, (u64)dst_capacity);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
     return 0;
 }

@@ -39,10 +39,12 @@ __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
     *it = q;
 }
 
-// pieces (index >= pbase) whose first byte is in [lo, hi) (origin-relative) get `val`
-__device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 lo, u64 hi, u64 val) {
+// pieces whose first byte is in [lo, hi) (origin-relative) get `val`; only pieces of the
+// batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the
+// batch unordered, and its pointers are clipped here)
+__device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u64 val) {
     u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
-    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi; ++p) *gptr<u64>(ptr + (p - pbase)) = val;
+    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi && p < pend; ++p) *gptr<u64>(ptr + (p - pbase)) = val;
 }
 
 __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned char* __restrict__ buf,
@@ -57,6 +59,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
     const u32 s = blockIdx.x * PWALK_T + threadIdx.x;
     if (s >= nseg) return;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const u64 pend = hi + lead0 ? ((hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
     const u64 so = seg_off[s], sl = seg_len[s];
     const u64 prev_end = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
     // out of order, or outside the declared range: the gated walker decodes the batch instead
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
     const u64 ibase = (u64)s * max_frames;
     const u64 sorg = so + lead0;                                            // origin-relative segment start
     const u64 tag = (u64)s << 32;
-    put_ptrs(ptr, pbase, s ? prev_end + lead0 : 0, sorg, tag);                     // pieces starting in the gap before s
+    put_ptrs(ptr, pbase, pend, s ? prev_end + lead0 : 0, sorg, tag);                     // pieces starting in the gap before s
     u64 off = 0, walked_end = sorg;
     u32 nf = 0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
         walked_end = p0 + h.plen;                                            // frame extent (ret may truncate)
         // item k = nf: the payload range if masked, else an empty range at the payload start
         put_item(gptr<u32x4>(items + ibase + nf), p0, h.masked ? walked_end : p0, rotl32(h.key, 8u * (u32)(p0 & 3)));
-        put_ptrs(ptr, pbase, fo, walked_end, tag | nf);                             // pieces starting inside this frame
+        put_ptrs(ptr, pbase, pend, fo, walked_end, tag | nf);                             // pieces starting inside this frame
         if (h.ret == 0) { extra = 1; break; }                                // (int) truncated to 0: unmasked,
         ws_store_desc(desc + dbase + nf, so + off, h);                       // no descriptor, loop breaks
         ++nf;
@@ -100,8 +103,8 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
         p = pn;
     }
     const u32 cnt = nf + extra;
-    put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);                         // pieces starting in the tail
-    if (s == nseg - 1) put_ptrs(ptr, pbase, sorg + sl, hi + lead0, PIECE_NONE);      // after the last segment
+    put_ptrs(ptr, pbase, pend, walked_end, sorg + sl, tag | cnt);                         // pieces starting in the tail
+    if (s == nseg - 1) put_ptrs(ptr, pbase, pend, sorg + sl, hi + lead0, PIECE_NONE);      // after the last segment
     ws_store_res(res + s, off, nf, status);
     *gptr<u32>(nwork + s) = cnt;
 }
@@ -130,6 +133,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     bool active = s < nseg;
     const u32 sc = active ? s : nseg - 1;                                    // inactive groups: harmless loads
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const u64 pend = hi + lead0 ? ((hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
     const u64 so = seg_off[sc], sl = seg_len[sc];
     const u64 prev_end = sc ? seg_off[sc - 1] + seg_len[sc - 1] : 0;
     if (active && gl == 0 && (prev_end > so || so < lo || sl > hi - so)) *gptr<u32>(disorder) = gen;
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     const u64 sorg = so + lead0;
     const u64 tag = (u64)sc << 32;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(buf + so);
-    if (active && gl == 0) put_ptrs(ptr, pbase, s ? prev_end + lead0 : 0, sorg, tag);
+    if (active && gl == 0) put_ptrs(ptr, pbase, pend, s ? prev_end + lead0 : 0, sorg, tag);
     u64 off = 0, g = 0, walked_end = sorg;
     u32 nf = 0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
@@ -179,7 +183,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         if (gl < ntake) {                                                   // consumed frames, in parallel
             put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0,
                      rotl32(h.key, 8u * (u32)(p0 & 3)));
-            put_ptrs(ptr, pbase, fo, fe, tag | (nf + gl));
+            put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
             if (h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
         }
         const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
@@ -207,8 +211,8 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         active = false;
         if (gl == 0) {
             const u32 cnt = nf + extra;
-            put_ptrs(ptr, pbase, walked_end, sorg + sl, tag | cnt);         // pieces starting in the tail
-            if (s == nseg - 1) put_ptrs(ptr, pbase, sorg + sl, hi + lead0, PIECE_NONE);
+            put_ptrs(ptr, pbase, pend, walked_end, sorg + sl, tag | cnt);         // pieces starting in the tail
+            if (s == nseg - 1) put_ptrs(ptr, pbase, pend, sorg + sl, hi + lead0, PIECE_NONE);
             ws_store_res(res + s, off, nf, status);
             *gptr<u32>(nwork + s) = cnt;
         }
@@ -332,31 +336,49 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 // fallback walker compares with `gen`.
 int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3: 64/32/16 lanes per segment
 
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out) {
+// K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
+int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
-    const u64 npieces = piece_count(lo_org, hi_org);
-    const u64 pbase = lo_org >> PIECE_SHIFT;
-    const u64 c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
-    u32* disorder = reinterpret_cast<u32*>(ws);
-    u64* ptr = reinterpret_cast<u64*>(ws + 16);
-    size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
-    u32* nwork = reinterpret_cast<u32*>(ws + b);
+    PieceWs P;
+    P.npieces = piece_count(lo_org, hi_org);
+    P.pbase = lo_org >> PIECE_SHIFT;
+    P.c_lo = lo_org >> 4;
+    P.c_hi = (hi_org + 15) >> 4;
+    P.disorder = reinterpret_cast<u32*>(ws);
+    P.ptr = reinterpret_cast<u64*>(ws + 16);
+    size_t b = (16 + P.npieces * 8 + 15) & ~(size_t)15;
+    P.nwork = reinterpret_cast<u32*>(ws + b);
     b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
-    u32x4* items = reinterpret_cast<u32x4*>(ws + b);
-    hipError_t e;
+    P.items = reinterpret_cast<u32x4*>(ws + b);
     if (ws_piece_scan >= 1 && ws_piece_scan <= 3) {
         const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : 16);
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
         auto k = G == 64 ? ws_piece_scan_kernel<64> : (G == 32 ? ws_piece_scan_kernel<32> : ws_piece_scan_kernel<16>);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                           L.max_frames, L.desc_base, L.desc, L.res, items, nwork, ptr, disorder, gen, pbase, lo, hi);
-    }
-    else
+                           L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr, P.disorder, gen,
+                           P.pbase, lo, hi);
+    } else {
         hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
-                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, items, nwork,
-                           ptr, disorder, gen, pbase, lo, hi);
-    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_walk_kernel launch", e);
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items,
+                           P.nwork, P.ptr, P.disorder, gen, P.pbase, lo, hi);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
+    *out = P;
+    return 0;
+}
+
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out) {
+    PieceWs P;
+    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P);
+    if (rc) return rc;
+    hipError_t e;
+    const u64 npieces = P.npieces, pbase = P.pbase, c_lo = P.c_lo, c_hi = P.c_hi;
+    u32* disorder = P.disorder;
+    u64* ptr = P.ptr;
+    u32* nwork = P.nwork;
+    u32x4* items = P.items;
     if (npieces) {
         if (nt == 1)
             hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,

@@ -1,0 +1,185 @@
+// ws_reasm.hip — fused decode + fragmented-message reassembly (SURVEY §8a row a6,
+// §8f rank 1). The reactor-side behaviour: every decoded frame's
+// unmasked body joins the connection's pending message; a frame with FIN set closes
+// it, and the message body handed to the application is the concatenation of its
+// frames' bodies (a FIN frame with nothing pending is a message by itself). The
+// reference pays an unmask in place, a copy into a cached packet and a merge copy
+// (≈3x the bytes); here every body byte is read once from the wire and written once,
+// unmasked, into a contiguous per-connection output region.
+//
+// R1 ws_piece_scan_kernel (ws_piece.hip): the reactor-loop walk — descriptors,
+//    segment results, per-frame payload items.
+// R2 ws_reasm_layout_kernel: one thread per segment turns its descriptors into body
+//    placements (output offset = running sum of the bodies before it) and message
+//    descriptors, and carries the open/closed state across batches.
+// R3 ws_reasm_gather_kernel: one wavefront per frame body: 16-B-aligned output chunks
+//    from one unaligned 16-B wire load each, XOR with the key rotated to the output
+//    phase; the <=15 bytes at each body edge by byte ops (bodies are adjacent, so two
+//    waves may share an output chunk but never a byte).
+// The wire buffer is only read.
+#include "ws_common.h"
+
+#define RLAY_T 256
+#define RGAT_T 256
+#define RGAT_U 4
+
+struct GatherRec {       // 32 B per body, slot s*max_frames + body index
+    u64 src;             // first payload byte, origin-relative in the wire buffer
+    u64 dst;             // first body byte, origin-relative in the output buffer
+    u64 len;
+    u32 key;             // XOR key rotated to the output byte phase: byte (y & 3) for output byte y
+    u32 pad;
+};
+
+__global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
+    const unsigned char* __restrict__ buf, u32 nseg, u32 max_frames, const u64* __restrict__ seg_off,
+    const u64* __restrict__ seg_len, const WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
+    const u32x4* __restrict__ items, const unsigned char* __restrict__ out, const u64* __restrict__ out_off,
+    WebsocketMsgDesc_t* __restrict__ msg, u32* __restrict__ nmsg, unsigned char* __restrict__ open_io,
+    GatherRec* __restrict__ recs, u32* __restrict__ nbody) {
+    const u32 s = blockIdx.x * RLAY_T + threadIdx.x;
+    if (s >= nseg) return;
+    const u64 lead_o = reinterpret_cast<uintptr_t>(out) & 15;
+    const u64 so = seg_off[s], sl = seg_len[s];
+    const u64 ob = out_off ? out_off[s] : so;                               // output region start (d_out-relative)
+    const u64 base = (u64)s * max_frames;
+    const u32 nf = res[s].n_frames;
+    u32 open = open_io ? open_io[s] : 0u, cont = open;
+    u32 nm = 0, nb = 0, first = 0;
+    u64 q = 0, q0 = 0;
+    int status = res[s].status;
+    (void)buf;
+    for (u32 k = 0; k < nf; ++k) {
+        const WebsocketFrameDesc_t d = desc[base + k];
+        if (d.ret <= 0) break;                                               // the error frame has no body
+        const u64 len = d.datalen;
+        if (len > sl - q) { status = WEBSOCKET_SEG_ERR_OUT_SPACE; break; }  // only via the (int) return quirk
+        const u32x4 it = items[base + k];
+        const u64 w0 = (u64)it.x | ((u64)it.y << 32), w1 = (u64)it.z | ((u64)it.w << 32);
+        const u64 p0 = w0 & 0xFFFFFFFFFFFFull;
+        const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);            // key rotated to the wire phase
+        const u32 sh = 8u * (u32)(p0 & 3);
+        const u32 key = sh ? (rk >> sh) | (rk << (32 - sh)) : rk;           // the frame's key (wire order)
+        const u64 dst = ob + q + lead_o;
+        GatherRec r;
+        r.src = p0;
+        r.dst = dst;
+        r.len = len;
+        r.key = d.masked ? rotl32(key, 8u * (u32)(dst & 3)) : 0u;
+        r.pad = 0;
+        recs[base + nb++] = r;
+        q += len;
+        open = 1;
+        if (d.is_fin) {                                                      // the message is complete
+            WebsocketMsgDesc_t m;
+            m.out_off = ob + q0; m.len = q - q0; m.first_frame = first; m.n_frames = k + 1 - first;
+            m.complete = 1; m.continued = cont;
+            msg[base + nm++] = m;
+            first = k + 1;
+            q0 = q;
+            cont = 0;
+            open = 0;
+        }
+    }
+    if (open && nb > first) {                                                // still open at the segment end
+        WebsocketMsgDesc_t m;
+        m.out_off = ob + q0; m.len = q - q0; m.first_frame = first; m.n_frames = nb - first;
+        m.complete = 0; m.continued = cont;
+        msg[base + nm++] = m;
+    }
+    if (status != res[s].status) res[s].status = status;
+    nmsg[s] = nm;
+    nbody[s] = nb;
+    if (open_io) open_io[s] = (unsigned char)open;
+}
+
+typedef u32x4 __attribute__((aligned(1))) u32x4u;
+
+template <int NT>
+__global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned char* __restrict__ buf,
+                                                                 unsigned char* __restrict__ out, u32 max_frames,
+                                                                 u64 nslots, const GatherRec* __restrict__ recs,
+                                                                 const u32* __restrict__ nbody) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 nw = (u64)gridDim.x * (RGAT_T / 64);
+    const uintptr_t borg = reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15;
+    const uintptr_t oorg = reinterpret_cast<uintptr_t>(out) & ~(uintptr_t)15;
+    for (u64 slot = (u64)blockIdx.x * (RGAT_T / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); slot < nslots;
+         slot += nw) {
+        const u32 s = (u32)(slot / max_frames), k = (u32)(slot - (u64)s * max_frames);
+        if (k >= *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(nbody + s))) continue;
+        const __attribute__((address_space(4))) u32* rq =
+            reinterpret_cast<const __attribute__((address_space(4))) u32*>(reinterpret_cast<uintptr_t>(recs + slot));
+        const u64 src = (u64)rq[0] | ((u64)rq[1] << 32), dst = (u64)rq[2] | ((u64)rq[3] << 32);
+        const u64 len = (u64)rq[4] | ((u64)rq[5] << 32);
+        const u32 key = rq[6];
+        if (!len) continue;
+        const u64 d1 = dst + len;
+        const u64 A = (dst + 15) & ~15ull, B = d1 & ~15ull;
+        // edge bytes: lanes 0-15 the head [dst, min(A, d1)), lanes 16-31 the tail [max(A, B), d1)
+        u64 y = 0;
+        bool act = false;
+        if (lane < 16) { y = dst + lane; act = y < (A < d1 ? A : d1); }
+        else if (lane < 32) { y = (A > B ? A : B) + (lane - 16); act = y < d1; }
+        const u32 eb = *reinterpret_cast<const gu8*>(borg + src + (act ? y - dst : 0));
+        // interior: 16-B output chunks [A, B)
+        if (A < B) {
+            const u64 nch = (B - A) >> 4;
+            for (u64 c0 = 0; c0 < nch; c0 += 64 * RGAT_U) {
+                u32x4 v[RGAT_U];
+#pragma unroll
+                for (int u = 0; u < RGAT_U; ++u) {
+                    const u64 c = c0 + (u64)(u * 64 + lane);
+                    const u64 cc = c < nch ? c : nch - 1;
+                    v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(borg + src + (A + (cc << 4) - dst));
+                }
+#pragma unroll
+                for (int u = 0; u < RGAT_U; ++u) {
+                    const u64 c = c0 + (u64)(u * 64 + lane);
+                    if (c < nch) st16<NT>(v[u] ^ key, reinterpret_cast<gu32x4*>(oorg + A + (c << 4)));
+                }
+            }
+        }
+        if (act) *reinterpret_cast<gu8*>(oorg + y) = (unsigned char)(eb ^ (key >> (8u * (u32)(y & 3))));
+    }
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
+    const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
+    unsigned int nseg, unsigned int max_frames, WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
+    unsigned char* d_out, const u64* d_out_off, WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
+    unsigned char* d_open, void* hip_stream) {
+    if (nseg == 0) return 0;
+    if (!d_buf || !d_seg_off || !d_seg_len || !d_desc || !d_res || !d_out || !d_msg || !d_nmsg || max_frames == 0)
+        return ws_set_msg("websocketframeBatchReassembleDevice: invalid argument");
+    if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_res) | reinterpret_cast<uintptr_t>(d_msg)) & 15)
+        return ws_set_msg("websocketframeBatchReassembleDevice: d_desc/d_res/d_msg not 16-B aligned");
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    const u64 nslots = (u64)nseg * max_frames;
+    const size_t piece = ws_piece_workspace_bytes(buflen, nseg, max_frames);
+    const size_t rec_off = (piece + 255) & ~(size_t)255;
+    const size_t nb_off = rec_off + nslots * sizeof(GatherRec);
+    void* ws = nullptr;
+    int rc = ws_device_workspace(nb_off + (size_t)nseg * 4 + 64, st, &ws);
+    if (rc) return rc;
+    unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
+    GatherRec* recs = reinterpret_cast<GatherRec*>(w8 + rec_off);
+    u32* nbody = reinterpret_cast<u32*>(w8 + nb_off);
+    WsLaunch L;
+    L.buf = const_cast<unsigned char*>(d_buf); L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg;
+    L.max_frames = max_frames; L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
+    PieceWs P;
+    if ((rc = ws_launch_piece_scan(L, 0, buflen, w8, ws_next_gen(), &P))) return rc;
+    hipLaunchKernelGGL(ws_reasm_layout_kernel, dim3((nseg + RLAY_T - 1) / RLAY_T), dim3(RLAY_T), 0, st, d_buf, nseg,
+                       max_frames, d_seg_off, d_seg_len, d_desc, d_res, P.items, d_out, d_out_off, d_msg, d_nmsg,
+                       d_open, recs, nbody);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ws_set_err("ws_reasm_layout_kernel launch", e);
+    const u64 waves = nslots;
+    const u64 blocks = (waves + RGAT_T / 64 - 1) / (RGAT_T / 64);
+    const u32 grid = (u32)(blocks < (1ull << 20) ? blocks : (1ull << 20));
+    hipLaunchKernelGGL((ws_reasm_gather_kernel<1>), dim3(grid), dim3(RGAT_T), 0, st, d_buf, d_out, max_frames, nslots,
+                       recs, nbody);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_reasm_gather_kernel launch", e);
+    return 0;
+}

@@ -21,12 +21,16 @@ WEBSOCKET_PONG_FRAME = 10
 WEBSOCKET_MAX_ENCODE_HEADLENGTH = 10
 
 SEG_OK, SEG_MAX_FRAMES, SEG_ERR_DECODE, SEG_ERR_LEN_WRAP = 0, 1, -1, -2
+SEG_ERR_OUT_SPACE = -3
 DATA_OFF_NULL = 0xFFFFFFFFFFFFFFFF
 BATCH_PAD = 32  # WEBSOCKET_BATCH_PAD: readable device bytes required after every segment
 
 DESC_DTYPE = np.dtype([("frame_off", "<u8"), ("data_off", "<u8"), ("datalen", "<u8"), ("ret", "<i4"),
                        ("is_fin", "u1"), ("type", "u1"), ("masked", "u1"), ("hdrlen", "u1")])
 SEGRES_DTYPE = np.dtype([("consumed", "<u8"), ("n_frames", "<u4"), ("status", "<i4")])
+MSG_DTYPE = np.dtype([("out_off", "<u8"), ("len", "<u8"), ("first_frame", "<u4"), ("n_frames", "<u4"),
+                      ("complete", "<u4"), ("continued", "<u4")])
+assert MSG_DTYPE.itemsize == 32
 ENC_DTYPE = np.dtype([("src_off", "<u8"), ("len", "<u8"), ("mask_key", "<u4"), ("type", "u1"), ("is_fin", "u1"),
                       ("prev_is_fin", "u1"), ("masked", "u1")])
 assert ENC_DTYPE.itemsize == 24
@@ -139,6 +143,20 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
                                                     nseg, max_frames, _ptr(desc_base), _ptr(desc), _ptr(res),
                                                     _stream(stream))
     check(rc, "websocketframeBatchDecodeDevice")
+
+
+def batch_reassemble_device(buf, seg_off, seg_len, max_frames, desc, res, out, msg, nmsg, out_off=None, open_state=None,
+                            stream=None):
+    """websocketframeBatchReassembleDevice on torch CUDA tensors: buf (uint8, wire, read only;
+    the last BATCH_PAD bytes are slack), seg_off/seg_len/out_off (int64), desc (uint8
+    >= 32*nseg*max_frames), res (uint8 16*nseg), out (uint8), msg (uint8 >= 32*nseg*max_frames),
+    nmsg (int32 nseg), open_state (uint8 nseg, in/out, optional); async on `stream`."""
+    nseg = seg_off.numel()
+    assert buf.numel() >= BATCH_PAD and seg_len.numel() == nseg and nmsg.numel() >= nseg
+    rc = load_lib().websocketframeBatchReassembleDevice(
+        _ptr(buf), buf.numel() - BATCH_PAD, _ptr(seg_off), _ptr(seg_len), nseg, max_frames, _ptr(desc), _ptr(res),
+        _ptr(out), _ptr(out_off), _ptr(msg), _ptr(nmsg), _ptr(open_state), _stream(stream))
+    check(rc, "websocketframeBatchReassembleDevice")
 
 
 def batch_encode_device(src, frames, dst, wire_off, capacity=None, stream=None):
