@@ -257,6 +257,81 @@ def run_encode(args, dev, world, rank):
     return mism
 
 
+def run_reasm(args, dev, world, rank):
+    """Fused decode + message reassembly: the wire stays in HBM
+    untouched, every message body is gathered unmasked into a contiguous output region.
+    Algorithmic bytes: read every wire byte + write every body byte (8,623,489,024 B at cfg5)."""
+    import torch
+    from util_amd import dist as D
+    from util_amd import wsframe as W
+    wl = Workload.make(args.config, dev, seed_offset=rank)
+    out = torch.empty(wl.wire_bytes + 64, dtype=torch.uint8, device=dev)
+    msg = torch.empty(wl.nseg * wl.fps * 32, dtype=torch.uint8, device=dev)
+    nmsg = torch.empty(wl.nseg, dtype=torch.int32, device=dev)
+
+    def step():
+        W.batch_reassemble_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res, out, msg, nmsg)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = D.allreduce([time.perf_counter() - t0], op="max", device=dev)[0]
+    kern_ms = np.array([a.elapsed_time(b) for a, b in zip(starts, ends)])
+    # check: the wire is still masked; decoding it in place must yield the gathered bodies
+    bad = int(wl.verify(expect_plain=False) != 0)
+    wl.decode()
+    t = torch
+    plen, hl = wl.plen_h, wl.wirelen_h - wl.plen_h
+    if wl.plen_kind == 0:                    # fixed-size frames: vectorised comparison
+        n, fl = wl.nframes, int(wl.wirelen_h[0])
+        bodies = wl.buf[:wl.wire_bytes].view(n, fl)[:, int(hl[0]):]
+        # output regions start at seg_off; bodies of a segment are back to back
+        seg_body = int(plen[0]) * wl.fps
+        outv = t.stack([out[int(o):int(o) + seg_body] for o in wl.seg_off_h[:64]])
+        bad += int(not t.equal(outv.view(-1, int(plen[0])), bodies[:64 * wl.fps]))
+        nm = nmsg.cpu().numpy()
+        bad += int(not (nm == (1 if wl.b0_kind == 2 else wl.fps)).all())
+    wl.decode()                              # back to the masked wire
+    mism = int(D.allreduce([bad], device=dev)[0])
+    mean_kern = float(kern_ms.mean()) / 1e3
+    algo = wl.wire_bytes + wl.payload_bytes
+    out_json = {
+        "metric": "WebSocket fused unmask + message reassembly GiB/s of bodies (device-resident)",
+        "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
+        "config": {"workload": "reassemble " + Workload.DESCRIPTION[args.config], "config": args.config,
+                   "frames_per_gpu": wl.nframes, "segments_per_gpu": wl.nseg, "wire_bytes_per_gpu": wl.wire_bytes,
+                   "payload_bytes_per_gpu": wl.payload_bytes},
+        "roofline": {"bound": "hbm", "achieved": round(algo / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(algo / mean_kern / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                     "kernel": "ws_reasm_gather_kernel", "algo_bytes_per_launch": algo,
+                     "timed": "HIP events around each call: ws_piece_scan_kernel + ws_reasm_layout_kernel + "
+                              "ws_reasm_gather_kernel",
+                     "kernel_ms_mean": round(mean_kern * 1e3, 4)},
+        "verified": mism == 0,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out_json), flush=True)
+    return mism
+
+
 def end_to_end(wl, runs=2):
     """websocketframeBatchDecodeHost on a pinned host copy of the whole batch: H2D + decode + D2H,
     pipelined over ~64 MiB segment groups on 3 streams (SURVEY §8d end-to-end). Reported beside
@@ -357,8 +432,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
-    ap.add_argument("--op", default="decode", choices=["decode", "encode"],
-                    help="decode (the headline) or client-side encode + mask of the same frames")
+    ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm"],
+                    help="decode (the headline), client-side encode + mask of the same frames, or fused "
+                         "decode + message reassembly (use with --config cfg5)")
     args = ap.parse_args()
     from util_amd import wsframe as W
     path = DEFAULT_PATH if args.path is None else args.path
@@ -375,8 +451,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.op == "encode":
-        mism = run_encode(args, dev, world, rank)
+    if args.op in ("encode", "reasm"):
+        mism = (run_encode if args.op == "encode" else run_reasm)(args, dev, world, rank)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)

@@ -150,6 +150,17 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
                                                      unsigned int max_frames, WebsocketFrameDesc_t* h_desc,
                                                      WebsocketSegResult_t* h_res, int device);
 
+/* One raw rx stream of any size (a single connection's inbuf; no frame offsets from the
+ * host): identical results to websocketframeBatchDecodeDevice with the one segment
+ * [0, len) (descriptors d_desc[0..], result d_res[0]); WEBSOCKET_BATCH_PAD readable bytes
+ * after d_buf + len. Frame boundaries are found by grid-wide speculative passes (one
+ * pass per change of frame length, each ends with an 8-byte device-to-host read), so
+ * the call synchronizes hip_stream; streams whose lengths keep changing finish in a
+ * single-wavefront walk. Returns 0 or a negative error. */
+WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,
+                                                        unsigned int max_frames, WebsocketFrameDesc_t* d_desc,
+                                                        WebsocketSegResult_t* d_res, void* hip_stream);
+
 /* Last HIP error string of the calling thread's most recent failed call ("" if none). */
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 

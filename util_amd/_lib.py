@@ -28,7 +28,7 @@ EXPORTS = [
     "websocketframeEncodeHandshakeResponse", "websocketframeEncodeHandshakeResponseWithProtocol",
     "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
     "websocketframeEncode", "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
-    "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice",
+    "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice", "websocketframeStreamDecodeDevice",
     "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuCalibrate", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
 ]
 
@@ -70,6 +70,8 @@ def load_lib():
     lib.websocketframeBatchDecodeDevice.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, vp, vp]
     lib.websocketframeBatchReassembleDevice.restype = i32
     lib.websocketframeBatchReassembleDevice.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.websocketframeStreamDecodeDevice.restype = i32
+    lib.websocketframeStreamDecodeDevice.argtypes = [vp, u64, u32, vp, vp, vp]
     lib.websocketframeBatchEncodeDevice.restype = i32
     lib.websocketframeBatchEncodeDevice.argtypes = [vp, vp, u32, vp, u64, vp, vp]
     lib.websocketframeBatchDecodeHost.restype = i32

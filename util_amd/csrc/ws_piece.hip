@@ -369,27 +369,27 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     return 0;
 }
 
+// K2 alone over the pieces of a scanned batch
+int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
+    if (!P.npieces) return 0;
+    if (nt == 1)
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf,
+                           L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
+                           P.c_lo, P.c_hi);
+    else
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<0>), dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf,
+                           L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
+                           P.c_lo, P.c_hi);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
+}
+
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out) {
     PieceWs P;
     int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P);
     if (rc) return rc;
-    hipError_t e;
-    const u64 npieces = P.npieces, pbase = P.pbase, c_lo = P.c_lo, c_hi = P.c_hi;
+    if ((rc = ws_launch_piece_unmask(L, P, nt, gen))) return rc;
     u32* disorder = P.disorder;
-    u64* ptr = P.ptr;
-    u32* nwork = P.nwork;
-    u32x4* items = P.items;
-    if (npieces) {
-        if (nt == 1)
-            hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, disorder, gen, pbase, c_lo,
-                               c_hi);
-        else
-            hipLaunchKernelGGL((ws_piece_unmask_kernel<0>), dim3((u32)npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                               L.seg_off, L.seg_len, L.nseg, L.max_frames, items, nwork, ptr, disorder, gen, pbase, c_lo,
-                               c_hi);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
-    }
     *disorder_out = disorder;
     return 0;
 }

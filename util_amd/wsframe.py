@@ -145,6 +145,15 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
     check(rc, "websocketframeBatchDecodeDevice")
 
 
+def stream_decode_device(buf, length, max_frames, desc, res, stream=None):
+    """websocketframeStreamDecodeDevice: one raw stream buf[0:length) (uint8 CUDA tensor with
+    >= BATCH_PAD bytes after it), decoded in place; synchronizes `stream`."""
+    assert buf.numel() >= length + BATCH_PAD
+    rc = load_lib().websocketframeStreamDecodeDevice(_ptr(buf), length, max_frames, _ptr(desc), _ptr(res),
+                                                     _stream(stream))
+    check(rc, "websocketframeStreamDecodeDevice")
+
+
 def batch_reassemble_device(buf, seg_off, seg_len, max_frames, desc, res, out, msg, nmsg, out_off=None, open_state=None,
                             stream=None):
     """websocketframeBatchReassembleDevice on torch CUDA tensors: buf (uint8, wire, read only;
