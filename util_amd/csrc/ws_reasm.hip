@@ -31,63 +31,106 @@ struct GatherRec {       // 32 B per body, slot s*max_frames + body index
     u32 pad;
 };
 
+// R2 with LG lanes per segment: lane j takes frame k0 + j of each round of LG frames;
+// body offsets are a group prefix sum, message boundaries come from the group's FIN mask.
+#define RLAY_G 16
 __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
     const unsigned char* __restrict__ buf, u32 nseg, u32 max_frames, const u64* __restrict__ seg_off,
     const u64* __restrict__ seg_len, const WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     const u32x4* __restrict__ items, const unsigned char* __restrict__ out, const u64* __restrict__ out_off,
     WebsocketMsgDesc_t* __restrict__ msg, u32* __restrict__ nmsg, unsigned char* __restrict__ open_io,
     GatherRec* __restrict__ recs, u32* __restrict__ nbody) {
-    const u32 s = blockIdx.x * RLAY_T + threadIdx.x;
-    if (s >= nseg) return;
+    constexpr u32 G = RLAY_G;
+    const u32 lane = threadIdx.x & 63, gl = lane % G, gb = lane - gl;
+    const u32 s = (blockIdx.x * RLAY_T + threadIdx.x) / G;
+    const bool active = s < nseg;
+    const u32 sc = active ? s : nseg - 1;
     const u64 lead_o = reinterpret_cast<uintptr_t>(out) & 15;
-    const u64 so = seg_off[s], sl = seg_len[s];
-    const u64 ob = out_off ? out_off[s] : so;                               // output region start (d_out-relative)
-    const u64 base = (u64)s * max_frames;
-    const u32 nf = res[s].n_frames;
-    u32 open = open_io ? open_io[s] : 0u, cont = open;
-    u32 nm = 0, nb = 0, first = 0;
+    const u64 so = seg_off[sc], sl = seg_len[sc];
+    const u64 ob = out_off ? out_off[sc] : so;                              // output region start (d_out-relative)
+    const u64 base = (u64)sc * max_frames;
+    const u32 nf = active ? res[sc].n_frames : 0u;
+    const int status0 = res[sc].status;
+    u32 open = active && open_io ? open_io[sc] : 0u, cont = open;
+    u32 nm = 0, nb = 0, first = 0;                                           // group-uniform state
     u64 q = 0, q0 = 0;
-    int status = res[s].status;
+    bool stop = false, overflow = false;
+    const u64 gmask = (1ull << G) - 1;
     (void)buf;
-    for (u32 k = 0; k < nf; ++k) {
-        const WebsocketFrameDesc_t d = desc[base + k];
-        if (d.ret <= 0) break;                                               // the error frame has no body
-        const u64 len = d.datalen;
-        if (len > sl - q) { status = WEBSOCKET_SEG_ERR_OUT_SPACE; break; }  // only via the (int) return quirk
-        const u32x4 it = items[base + k];
-        const u64 w0 = (u64)it.x | ((u64)it.y << 32), w1 = (u64)it.z | ((u64)it.w << 32);
-        const u64 p0 = w0 & 0xFFFFFFFFFFFFull;
-        const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);            // key rotated to the wire phase
-        const u32 sh = 8u * (u32)(p0 & 3);
-        const u32 key = sh ? (rk >> sh) | (rk << (32 - sh)) : rk;           // the frame's key (wire order)
-        const u64 dst = ob + q + lead_o;
-        GatherRec r;
-        r.src = p0;
-        r.dst = dst;
-        r.len = len;
-        r.key = d.masked ? rotl32(key, 8u * (u32)(dst & 3)) : 0u;
-        r.pad = 0;
-        recs[base + nb++] = r;
-        q += len;
-        open = 1;
-        if (d.is_fin) {                                                      // the message is complete
-            WebsocketMsgDesc_t m;
-            m.out_off = ob + q0; m.len = q - q0; m.first_frame = first; m.n_frames = k + 1 - first;
-            m.complete = 1; m.continued = cont;
-            msg[base + nm++] = m;
-            first = k + 1;
-            q0 = q;
-            cont = 0;
-            open = 0;
+    for (u32 k0 = 0; __ballot(active && !stop && k0 < nf); k0 += G) {
+        const u32 k = k0 + gl;
+        const bool in = active && !stop && k < nf;
+        WebsocketFrameDesc_t d = {};
+        u32x4 it = {0, 0, 0, 0};
+        if (in) { d = desc[base + k]; it = items[base + k]; }
+        // frames with a body: consecutive from k0 up to the first ret <= 0 (the error frame)
+        const u64 badm = (__ballot(in && d.ret <= 0) >> gb) & gmask;
+        const u64 inm = (__ballot(in) >> gb) & gmask;
+        const u32 nbody_r = badm ? (u32)__builtin_ctzll(badm) : (u32)__builtin_popcountll(inm);
+        const bool body = gl < nbody_r;
+        const u64 len = body ? d.datalen : 0;
+        // inclusive prefix sum of the body lengths within the group
+        u64 incl = len;
+#pragma unroll
+        for (u32 o = 1; o < G; o <<= 1) {
+            const u64 t = __shfl_up(incl, o, G);
+            if (gl >= o) incl += t;
         }
+        const u64 qs = q + incl - len;                                       // this body's output offset
+        // bodies must fit the segment's region (only the (int) return quirk can break this)
+        const u64 ovm = (__ballot(body && qs + len > sl) >> gb) & gmask;
+        const u32 ntake = ovm ? (u32)__builtin_ctzll(ovm) : nbody_r;
+        if (gl < ntake) {
+            const u64 p0 = ((u64)it.x | ((u64)it.y << 32)) & 0xFFFFFFFFFFFFull;
+            const u32 rk = (u32)(((u64)it.x | ((u64)it.y << 32)) >> 48) | ((u32)(((u64)it.z | ((u64)it.w << 32)) >> 48) << 16);
+            const u32 sh = 8u * (u32)(p0 & 3);
+            const u32 key = sh ? (rk >> sh) | (rk << (32 - sh)) : rk;       // the frame's key (wire order)
+            const u64 dst = ob + qs + lead_o;
+            GatherRec r;
+            r.src = p0; r.dst = dst; r.len = len; r.key = d.masked ? rotl32(key, 8u * (u32)(dst & 3)) : 0u; r.pad = 0;
+            recs[base + nb + gl] = r;
+        }
+        // messages closed by FIN frames among the taken ones
+        const u64 finm = (__ballot(gl < ntake && d.is_fin) >> gb) & gmask;
+        const u64 below = finm & ((1ull << gl) - 1);                         // earlier FINs in this round
+        const u32 prevl = below ? 63 - __builtin_clzll(below) : gl;
+        const u64 incl_prev = __shfl(incl, (int)(gb + prevl), 64);          // all lanes active here
+        if (gl < ntake && d.is_fin) {
+            const u32 mfirst = below ? k0 + prevl + 1 : first;
+            const u64 prevq = below ? q + incl_prev : q0;
+            WebsocketMsgDesc_t m;
+            m.out_off = ob + prevq; m.len = qs + len - prevq; m.first_frame = mfirst; m.n_frames = k + 1 - mfirst;
+            m.complete = 1; m.continued = below ? 0u : cont;
+            msg[base + nm + (u32)__builtin_popcountll(below)] = m;
+        }
+        const u64 tot_l = __shfl(incl, (int)(gb + (ntake ? ntake - 1 : 0)), 64);
+        const u32 last = finm ? 63 - __builtin_clzll(finm) : 0;             // last FIN of the round
+        const u64 incl_last = __shfl(incl, (int)(gb + last), 64);
+        const u64 tot = ntake ? tot_l : 0;
+        if (finm) {
+            q0 = q + incl_last;
+            first = k0 + last + 1;
+            cont = 0;
+            open = ntake > last + 1 ? 1u : 0u;
+            nm += (u32)__builtin_popcountll(finm);
+        } else if (ntake) {
+            open = 1;
+        }
+        q += tot;
+        nb += ntake;
+        if (ntake < G || k0 + G >= nf) stop = true;                          // error frame, overflow or end
+        if (ovm) overflow = true;
+        if (!active) stop = true;
     }
+    if (!active || gl != 0) return;
     if (open && nb > first) {                                                // still open at the segment end
         WebsocketMsgDesc_t m;
         m.out_off = ob + q0; m.len = q - q0; m.first_frame = first; m.n_frames = nb - first;
         m.complete = 0; m.continued = cont;
         msg[base + nm++] = m;
     }
-    if (status != res[s].status) res[s].status = status;
+    if (overflow) res[s].status = WEBSOCKET_SEG_ERR_OUT_SPACE;
+    (void)status0;
     nmsg[s] = nm;
     nbody[s] = nb;
     if (open_io) open_io[s] = (unsigned char)open;
@@ -129,6 +172,7 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
                 u32x4 v[RGAT_U];
 #pragma unroll
                 for (int u = 0; u < RGAT_U; ++u) {
+                    if (u && c0 + (u64)u * 64 >= nch) break;                 // wave-uniform: no empty rows
                     const u64 c = c0 + (u64)(u * 64 + lane);
                     const u64 cc = c < nch ? c : nch - 1;
                     v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(borg + src + (A + (cc << 4) - dst));
@@ -170,7 +214,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     L.max_frames = max_frames; L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
     PieceWs P;
     if ((rc = ws_launch_piece_scan(L, 0, buflen, w8, ws_next_gen(), &P))) return rc;
-    hipLaunchKernelGGL(ws_reasm_layout_kernel, dim3((nseg + RLAY_T - 1) / RLAY_T), dim3(RLAY_T), 0, st, d_buf, nseg,
+    hipLaunchKernelGGL(ws_reasm_layout_kernel, dim3((u32)(((u64)nseg * RLAY_G + RLAY_T - 1) / RLAY_T)), dim3(RLAY_T), 0, st, d_buf, nseg,
                        max_frames, d_seg_off, d_seg_len, d_desc, d_res, P.items, d_out, d_out_off, d_msg, d_nmsg,
                        d_open, recs, nbody);
     hipError_t e = hipGetLastError();
