@@ -257,6 +257,16 @@ def run_encode(args, dev, world, rank):
     return mism
 
 
+def reasm_fused(wl):
+    """websocketframeBatchReassembleDevice's path choice for this batch (ws_reasm.hip): the
+    fused per-segment kernel for >= 1024 segments of <= 256 KiB average, max_frames <= 64"""
+    opt = dict(kv.split("=") for kv in filter(None, os.environ.get("WSFRAME_AMD_OPTIONS", "").split(",")))
+    p = int(opt.get("reasm_path", 0))
+    if p:
+        return p == 1 and wl.fps <= 64
+    return wl.fps <= 64 and wl.nseg >= 1024 and wl.wire_bytes <= wl.nseg << 18
+
+
 def run_reasm(args, dev, world, rank):
     """Fused decode + message reassembly: the wire stays in HBM
     untouched, every message body is gathered unmasked into a contiguous output region.
@@ -308,6 +318,13 @@ def run_reasm(args, dev, world, rank):
     mism = int(D.allreduce([bad], device=dev)[0])
     mean_kern = float(kern_ms.mean()) / 1e3
     algo = wl.wire_bytes + wl.payload_bytes
+    fused = reasm_fused(wl)
+    kname = "ws_reasm_seg_kernel" if fused else "ws_reasm_gather_kernel"
+    pmc = pmc_traffic(kname, algo)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(wl.host_sample(262144), min(args.cpu_threads, os.cpu_count() or 1), op="reasm",
+                           frames_per_segment=wl.fps)
     out_json = {
         "metric": "WebSocket fused unmask + message reassembly GiB/s of bodies (device-resident)",
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
@@ -319,13 +336,17 @@ def run_reasm(args, dev, world, rank):
                    "frames_per_gpu": wl.nframes, "segments_per_gpu": wl.nseg, "wire_bytes_per_gpu": wl.wire_bytes,
                    "payload_bytes_per_gpu": wl.payload_bytes},
         "roofline": {"bound": "hbm", "achieved": round(algo / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": round(algo / mean_kern / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
-                     "kernel": "ws_reasm_gather_kernel", "algo_bytes_per_launch": algo,
-                     "timed": "HIP events around each call: ws_piece_scan_kernel + ws_reasm_layout_kernel + "
-                              "ws_reasm_gather_kernel",
+                     "unit": "GB/s", "frac": round(algo / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
+                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
+                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
+                     "kernel": kname,
+                     "algo_bytes_per_launch": algo,
+                     "timed": "HIP events around each call: " + (
+                         "ws_reasm_seg_kernel (one launch: decode + layout + gather per rx segment)" if fused else
+                         "ws_piece_scan_kernel + ws_reasm_layout_kernel + ws_reasm_gather_kernel"),
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out_json), flush=True)
@@ -364,17 +385,24 @@ def end_to_end(wl, runs=2):
             "path": "websocketframeBatchDecodeHost: H2D | decode | D2H over 64 MiB groups, 3 streams"}, runs + 1
 
 
-def cpu_baseline(sample, threads, min_seconds=1.0):
+def cpu_baseline(sample, threads, min_seconds=1.0, op="decode", frames_per_segment=16):
     """time the reference's own websocketframeDecode (oracle/_ref, reactor loop driver) —
-    or the oracle restatement when the reference build is absent — on host cores"""
+    or the oracle restatement when the reference build is absent — on host cores.
+    op "reasm": the same loop delivering messages as the reactor's stream hook does
+    (oracle/ref_loop.c:ref_reassemble_segments: packet cache + merge copies)."""
     buf, so, sl, payload = sample
     ref = os.path.join(REPO, "oracle", "_ref", "libwsref_loop.so")
+    what = "reactor loop net_reactor.c:515-526 over websocketframeDecode"
+    if op == "reasm":
+        if not os.path.exists(ref):
+            return None
+        what += " + fragment cache/merge delivery net_channel_ex.c:55-157 (restated glue)"
     if os.path.exists(ref):
         lib = C.CDLL(ref)
-        fn = lib.ref_decode_segments
+        fn = lib.ref_reassemble_segments if op == "reasm" else lib.ref_decode_segments
         fn.restype = C.c_ulonglong
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]
-        kind = "reference"
+        kind = "reference" if op == "decode" else "port"
 
         def run(lo, hi):
             nf = C.c_ulonglong()
@@ -418,8 +446,7 @@ def cpu_baseline(sample, threads, min_seconds=1.0):
             "single_thread_gibs": round(single, 3),
             "cpu_seconds": round(tn * threads + t1, 2),
             "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %d passes x %d threads, "
-                      "reactor loop net_reactor.c:515-526 over websocketframeDecode" %
-                      (nseg * 16, nseg, payload / 2**20, passes, threads)}
+                      "%s" % (nseg * frames_per_segment, nseg, payload / 2**20, passes, threads, what)}
 
 
 def main():

@@ -23,6 +23,15 @@ def dev():
     return torch.device("cuda:0")
 
 
+# reasm_path 1: fused one-workgroup-per-segment kernel (ws_reasm_seg_kernel, LDS windows),
+# 2: scan + layout + gather kernels; 0 (auto) picks by batch shape
+@pytest.fixture(params=[1, 2], ids=["fused", "three_kernel"], autouse=True)
+def reasm_path(request):
+    W.set_option("reasm_path", request.param)
+    yield request.param
+    W.set_option("reasm_path", 0)
+
+
 def gpu_reassemble(dev, wire, so, sl, max_frames, open_in=None, out_off=None, out_size=None):
     n = len(wire)
     d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
@@ -103,3 +112,85 @@ def test_reassemble_cfg5_shape(dev):
     wire = wl.buf[:wl.wire_bytes].cpu().numpy().copy()
     out, oms, _ = check(dev, wire, wl.seg_off_h, wl.seg_len_h, 16, tag="cfg5")
     assert all(len(m) == 1 and m[0][4] == 1 and m[0][1] == 16 * 1024 for m in oms)
+
+
+def _frame(rng, plen, masked=True, b0=0x82, form=None):
+    key = rng.integers(0, 256, 4, dtype=np.uint8) if masked else None
+    form = form or (7 if plen < 126 else (16 if plen <= 0xFFFF else 64))
+    h = bytearray([b0])
+    m = 0x80 if masked else 0
+    if form == 7:
+        h.append(m | plen)
+    elif form == 16:
+        h += bytes([m | 126]) + plen.to_bytes(2, "big")
+    else:
+        h += bytes([m | 127]) + plen.to_bytes(8, "big")
+    if masked:
+        h += key.tobytes()
+    return bytes(h) + rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+
+
+def _segments(parts_list, rng, gaps=True):
+    blob, so, sl = bytearray(), [], []
+    for parts in parts_list:
+        if gaps:
+            blob += bytes(int(rng.integers(0, 20)))
+        so.append(len(blob))
+        seg = b"".join(parts)
+        blob += seg
+        sl.append(len(seg))
+    return np.frombuffer(bytes(blob), dtype=np.uint8).copy(), so, sl
+
+
+def test_reassemble_frames_across_windows(dev):
+    """frames much longer than the fused kernel's 20 KiB LDS window, headers straddling
+    window edges, fragments with FIN only at the end, at every alignment"""
+    rng = np.random.default_rng(31)
+    segs = []
+    for i in range(64):
+        n = int(rng.integers(1, 8))
+        parts = []
+        for k in range(n):
+            plen = int(rng.choice([20475, 20470, 20480, 40960 + 3, 65536, 70000, 100, 0, 1]))
+            b0 = (0x80 if k == n - 1 else 0) | (2 if k == 0 else 0)
+            parts.append(_frame(rng, plen, masked=rng.random() < 0.9, b0=b0))
+        segs.append(parts)
+    wire, so, sl = _segments(segs, rng)
+    check(dev, wire, so, sl, 16, tag="windows")
+
+
+def test_reassemble_tiny_frames_max64(dev):
+    """many 0-3 byte bodies per segment (64 frames per walk round), max_frames 64"""
+    rng = np.random.default_rng(32)
+    segs = [[_frame(rng, int(rng.integers(0, 4)), masked=rng.random() < 0.8,
+                    b0=0x80 if rng.random() < 0.3 else 0) for _ in range(int(rng.integers(0, 90)))]
+            for _ in range(300)]
+    wire, so, sl = _segments(segs, rng)
+    check(dev, wire, so, sl, 64, tag="tiny")
+
+
+def test_reassemble_length_quirks(dev):
+    """u64 length wrap of an unmasked frame (websocketframe.c:149: consumed, body larger
+    than the segment -> WEBSOCKET_SEG_ERR_OUT_SPACE), masked wrap (fence), non-minimal
+    length forms, a ret < 0 frame is impossible below 2 GiB, so decode errors come only
+    from the fence"""
+    rng = np.random.default_rng(33)
+    # 10 + len wraps to 4: the reactor consumes 4 bytes and walks on inside the header
+    wrap = bytes([0x82, 127]) + ((1 << 64) - 6).to_bytes(8, "big") + bytes(range(14))
+    mwrap = bytes([0x82, 0xFF]) + ((1 << 64) - 14 + 5).to_bytes(8, "big") + bytes(range(14))
+    segs = []
+    for i in range(200):
+        parts = []
+        for _ in range(int(rng.integers(0, 5))):
+            plen = int(rng.integers(0, 300))
+            forms = [7, 16, 64] if plen < 126 else [16, 64]
+            parts.append(_frame(rng, plen, form=int(rng.choice(forms)) if i % 3 else None))
+        if i % 4 == 1:
+            parts.insert(int(rng.integers(0, len(parts) + 1)), wrap)
+        if i % 4 == 2:
+            parts.insert(int(rng.integers(0, len(parts) + 1)), mwrap)
+        segs.append(parts)
+    wire, so, sl = _segments(segs, rng)
+    _, orr, _, _, _ = oracle_reassemble(wire, so, sl, 16)
+    assert (orr["status"] == -3).any() and (orr["status"] == -2).any()
+    check(dev, wire, so, sl, 16, tag="quirks")

@@ -18,6 +18,7 @@ static __thread char g_last_error[256];
 extern int ws_dbg_flags;
 extern size_t ws_host_chunk_bytes;
 extern int ws_piece_scan;
+extern int ws_reasm_path;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -57,6 +58,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "blocks_per_cu")) g_tune.blocks_per_cu = (int)value;
     else if (!strcmp(name, "host_chunk_mb") && value > 0) ws_host_chunk_bytes = (size_t)value << 20;
     else if (!strcmp(name, "piece_scan")) ws_piece_scan = (int)value;
+    else if (!strcmp(name, "reasm_path")) ws_reasm_path = (int)value;
     else return -1;
     return 0;
 }

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
         }
         const u64 qs = q + incl - len;                                       // this body's output offset
         // bodies must fit the segment's region (only the (int) return quirk can break this)
-        const u64 ovm = (__ballot(body && qs + len > sl) >> gb) & gmask;
+        const u64 ovm = (__ballot(body && len > sl - qs) >> gb) & gmask;   // qs <= sl before the first overflow
         const u32 ntake = ovm ? (u32)__builtin_ctzll(ovm) : nbody_r;
         if (gl < ntake) {
             const u64 p0 = ((u64)it.x | ((u64)it.y << 32)) & 0xFFFFFFFFFFFFull;
@@ -188,6 +188,250 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused path: ONE workgroup per rx segment, the whole decode + reassembly of the segment
+// in one kernel. The segment's wire bytes stream through LDS in windows (one window for
+// segments up to 19 KiB: cfg5's 16.5 KiB messages are one-shot blocks — load once,
+// store once, exit, the pattern that reaches the part's streaming ceiling):
+//   1. LDS-DMA (global_load_lds_dwordx4): every wave issues its 1 KiB slices of the
+//      window at once, clamped to the segment's readable bytes (segment +
+//      WEBSOCKET_BATCH_PAD), no registers involved;
+//   2. wave 0 walks the reactor loop (net_reactor.c:515-526) over the headers in LDS by
+//      stride speculation (64 candidate frames per round, the stride seeded by the
+//      first header, as ws_piece_scan_kernel), writes the descriptors, places each body
+//      at the running sum of the bodies before it and emits the message descriptors
+//      (the delivery rule of SURVEY §8a a6);
+//   3. wave w copies bodies w, w+4, ... of the window: every 16-B-aligned output chunk
+//      inside a body is one unaligned 16-B LDS read (two aligned reads + funnel shift),
+//      XOR with the key rotated to the output phase, one 16-B store; the <= 15 bytes at
+//      each body/window edge go one per lane (lanes 0-15 head, 16-31 tail).
+// Frames longer than a window (or a header past it) continue in the next window; the
+// walk state and the body table (max_frames <= RSEG_TB bodies) persist across windows.
+// Each wire byte is read from HBM once (+ 1 KiB of look-ahead per extra window), each
+// body byte written once.
+#define RSEG_T 256
+#define RSEG_L 20                                  // LDS-DMA wave instructions per window (1 KiB each)
+#define RSEG_C ((RSEG_L - 1) * 64)                 // chunks owned per window: 19 KiB (+1 KiB look-ahead)
+#define RSEG_TB 64                                 // body table entries = max max_frames of this path
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct BodyL {           // body table entry (LDS)
+    u64 x0;              // first payload byte, window coordinates (segment offset + lead)
+    u64 dst;             // first body byte, region-relative
+    u64 len;
+    u32 key;             // key rotated to the absolute output phase (0 for unmasked frames)
+    u32 pad;
+};
+
+__global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
+    const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
+    const u64* __restrict__ seg_len, WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
+    unsigned char* __restrict__ out, const u64* __restrict__ out_off, WebsocketMsgDesc_t* __restrict__ msg,
+    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io) {
+    __shared__ __attribute__((aligned(16))) u32x4 win[RSEG_L * 64];
+    __shared__ BodyL tab[RSEG_TB];
+    __shared__ u64 sh_next;                        // next window's first chunk, ~0 = done
+    __shared__ u32 sh_blo, sh_bhi;                 // bodies with bytes in this window [blo, bhi], blo > bhi: none
+    const u32 s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool w0 = wv == 0;
+    const u64 so = seg_off[s], sl = seg_len[s];
+    const uintptr_t segp = reinterpret_cast<uintptr_t>(buf + so);
+    const u64 lead = segp & 15;
+    const gu32x4* const gseg = reinterpret_cast<const gu32x4*>(segp & ~(uintptr_t)15);
+    const u64 cmax = (sl + lead + WEBSOCKET_BATCH_PAD - 1) >> 4;     // last readable chunk
+    const u64 ob = out_off ? out_off[s] : so;
+    const uintptr_t obase = reinterpret_cast<uintptr_t>(out) + ob;   // absolute region start
+    const u64 base = (u64)s * max_frames;
+    const unsigned char* const wb = reinterpret_cast<const unsigned char*>(win);
+    // wave-0 walk state (wave-uniform)
+    u64 off = 0, g = 0, q = 0, q0 = 0;
+    u32 nf = 0, nb = 0, nm = 0, first = 0;
+    int status = WEBSOCKET_SEG_OK;
+    bool walking = true, bodies_on = true, overflow = false;
+    u32 open = w0 && open_io ? open_io[s] : 0u, cont = open;
+    u64 wc = 0;                                                      // window's first chunk
+    for (;;) {
+        const u64 W0 = wc << 4, W1 = W0 + (u64)RSEG_C * 16;
+        // ---- 1. LDS-DMA of the window (slices past the readable end are skipped)
+        for (u32 i = wv; i < RSEG_L; i += RSEG_T / 64) {
+            const u64 c0 = wc + (u64)i * 64;
+            if (c0 > cmax) break;
+            const u64 c = c0 + lane < cmax ? c0 + lane : cmax;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const WS_GLOBAL void*>(gseg + c),
+                                             (lds_void*)(&win[i * 64]), 16, 0, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // ---- 2. wave 0: headers starting in [W0, W1)
+        if (w0) {
+            while (walking) {
+                // stride seed: the length of the frame at `off` (speculation verified below)
+                if (g == 0 && off + lead < W1 && off < sl) {
+                    const u32 o = (u32)(off + lead - W0);
+                    u64 h0, h1;
+                    ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
+                    const WsHdr h = ws_parse(h0, h1, sl - off);
+                    if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
+                }
+                const u64 pos = off + (u64)lane * g;
+                const bool cand = lane == 0 || g > 0;
+                const u64 X = pos + lead;
+                const bool inwin = X < W1;
+                const bool eval = cand && pos < sl && inwin;
+                const u32 o = eval ? (u32)(X - W0) : 0u;
+                u64 h0, h1;
+                ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
+                const WsHdr h = ws_parse(h0, h1, eval ? sl - pos : 0);
+                // 0 consumed, chain continues  1 consumed, new stride  2 consumed, walk ends (ret <= 0)
+                // 3 not consumed, walk ends    4 header past this window: continue in the next one
+                u32 code = 3;
+                int st = WEBSOCKET_SEG_OK;
+                if (cand) {
+                    if (pos >= sl) code = 3;
+                    else if (nf + lane >= max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
+                    else if (!inwin) code = 4;
+                    else if (sl - pos < 2) code = 3;                          // websocketframe.c:121
+                    else if (h.kind == WS_PARSE_INCOMPLETE) code = 3;
+                    else if (h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
+                    else if (h.ret <= 0) { code = 2; st = h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
+                    else code = (u64)(u32)h.ret == g ? 0u : 1u;
+                }
+                const u64 stop = __ballot(code != 0);
+                const u32 mm = stop ? (u32)__builtin_ctzll(stop) : 64u;
+                const u32 src = mm < 64 ? mm : 63;
+                const u32 code_m = mm < 64 ? (u32)__shfl((int)code, (int)src) : 0u;
+                const int ret_m = __shfl(h.ret, (int)src);
+                const int st_m = __shfl(st, (int)src);
+                const u32 ntake = mm + ((code_m == 1 || code_m == 2) ? 1u : 0u);
+                if (lane < ntake && h.ret != 0) ws_store_desc(desc + base + nf + lane, so + pos, h);
+                // bodies: consumed frames with ret > 0 (the a6 delivery rule), each at the
+                // running sum of the bodies before it; none after an overflow
+                const u32 nbr = bodies_on ? mm + (code_m == 1 ? 1u : 0u) : 0u;
+                if (nbr) {
+                    const bool body = lane < nbr;
+                    const u64 len = body ? h.plen : 0;
+                    u64 incl = len;
+#pragma unroll
+                    for (u32 d = 1; d < 64; d <<= 1) {
+                        const u64 t = __shfl_up(incl, d, 64);
+                        if (lane >= d) incl += t;
+                    }
+                    const u64 qs = q + incl - len;
+                    // bodies must fit the segment's region (qs <= sl for every lane before the first overflow)
+                    const u64 ovm = __ballot(body && len > sl - qs);
+                    const u32 ntb = ovm ? (u32)__builtin_ctzll(ovm) : nbr;
+                    if (ovm) { bodies_on = false; overflow = true; }
+                    if (lane < ntb) {
+                        BodyL b;
+                        b.x0 = X + h.hdr; b.dst = qs; b.len = len;
+                        b.key = h.masked ? rotl32(h.key, 8u * (u32)((obase + qs) & 3)) : 0u; b.pad = 0;
+                        tab[nb + lane] = b;
+                    }
+                    // messages closed by FIN frames among the taken bodies (body index == frame index)
+                    const bool fin = lane < ntb && (h.b0 >> 7);
+                    const u64 finm = __ballot(fin);
+                    const u64 below = finm & ((1ull << lane) - 1);
+                    const u32 prevl = below ? 63 - __builtin_clzll(below) : lane;
+                    const u64 incl_prev = __shfl(incl, (int)prevl, 64);
+                    if (fin) {
+                        WebsocketMsgDesc_t m;
+                        const u32 mfirst = below ? nb + prevl + 1 : first;
+                        const u64 prevq = below ? q + incl_prev : q0;
+                        m.out_off = ob + prevq; m.len = qs + len - prevq; m.first_frame = mfirst;
+                        m.n_frames = nb + lane + 1 - mfirst; m.complete = 1; m.continued = below ? 0u : cont;
+                        msg[base + nm + (u32)__builtin_popcountll(below)] = m;
+                    }
+                    const u64 tot = __shfl(incl, (int)(ntb ? ntb - 1 : 0), 64);
+                    const u32 last = finm ? 63 - __builtin_clzll(finm) : 0;
+                    const u64 incl_last = __shfl(incl, (int)last, 64);
+                    if (finm) {
+                        q0 = q + incl_last;
+                        first = nb + last + 1;
+                        cont = 0;
+                        open = ntb > last + 1 ? 1u : 0u;
+                        nm += (u32)__builtin_popcountll(finm);
+                    } else if (ntb) {
+                        open = 1;
+                    }
+                    q += ntb ? tot : 0;
+                    nb += ntb;
+                }
+                // advance the reactor loop
+                if (mm == 64) { nf += 64; off += 64 * g; continue; }
+                const u64 pos_m = off + (u64)mm * g;
+                nf += mm;
+                if (code_m == 1) { nf += 1; off = pos_m + (u32)ret_m; g = (u32)ret_m; continue; }
+                off = pos_m;
+                if (code_m == 4) break;                                      // next header: next window
+                if (code_m == 2 && ret_m != 0) nf += 1;                      // ret < 0 keeps its descriptor
+                status = st_m;
+                walking = false;
+            }
+            // bodies with bytes in [W0, W1), and where the next window starts
+            const BodyL t = tab[lane];
+            const u64 bm = __ballot(lane < nb && t.len && t.x0 < W1 && t.x0 + t.len > W0);
+            const u64 lend = nb ? tab[nb - 1].x0 + tab[nb - 1].len : 0;      // only the last body can pend
+            if (lane == 0) {
+                sh_blo = bm ? (u32)__builtin_ctzll(bm) : 1u;
+                sh_bhi = bm ? 63u - (u32)__builtin_clzll(bm) : 0u;
+                sh_next = lend > W1 ? W1 >> 4 : (walking ? (off + lead) >> 4 : ~0ull);
+            }
+        }
+        __syncthreads();
+        // ---- 3. wave wv: the window's part of bodies blo + wv, blo + wv + 4, ...
+        const u32 bhi = sh_bhi;
+        for (u32 bi = sh_blo + wv; bi <= bhi; bi += RSEG_T / 64) {
+            const BodyL b = tab[bi];
+            if (!b.len) continue;
+            const u64 xa = b.x0 > W0 ? b.x0 : W0, xe = b.x0 + b.len < W1 ? b.x0 + b.len : W1;
+            const u64 da = obase + b.dst + (xa - b.x0), de = da + (xe - xa);   // absolute output range
+            const u64 A = (da + 15) & ~15ull, B = de & ~15ull;
+            // interior: 16-B output chunks [A, B), source at xa + (y - da)
+            if (A < B) {
+                const u32 nch = (u32)((B - A) >> 4);
+                const u32 o0 = (u32)(xa - W0 + (A - da));
+                for (u32 c = lane; c < nch; c += 64) {
+                    const u32 o = o0 + (c << 4);
+                    u64 h0, h1;
+                    ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
+                    u32x4 w;
+                    w.x = (u32)h0 ^ b.key; w.y = (u32)(h0 >> 32) ^ b.key;
+                    w.z = (u32)h1 ^ b.key; w.w = (u32)(h1 >> 32) ^ b.key;
+                    st16<1>(w, reinterpret_cast<gu32x4*>(A + ((u64)c << 4)));
+                }
+            }
+            // edges: lanes 0-15 the head [da, min(A, de)), lanes 16-31 the tail [max(A, B), de)
+            u64 y = 0;
+            bool act = false;
+            if (lane < 16) { y = da + lane; act = y < (A < de ? A : de); }
+            else if (lane < 32) { y = (A > B ? A : B) + (lane - 16); act = y < de; }
+            if (act) {
+                const u32 kb = (b.key >> (8u * (u32)(y & 3))) & 0xFFu;
+                *reinterpret_cast<gu8*>(y) = (unsigned char)(wb[xa - W0 + (y - da)] ^ kb);
+            }
+        }
+        const u64 nxt = sh_next;
+        __syncthreads();                                                     // window LDS is reused
+        if (nxt == ~0ull) break;
+        wc = nxt;
+    }
+    if (tid != 0) return;
+    if (open && nb > first) {                                                // still open at the segment end
+        WebsocketMsgDesc_t m;
+        m.out_off = ob + q0; m.len = q - q0; m.first_frame = first; m.n_frames = nb - first;
+        m.complete = 0; m.continued = cont;
+        msg[base + nm++] = m;
+    }
+    ws_store_res(res + s, off, nf, overflow ? WEBSOCKET_SEG_ERR_OUT_SPACE : status);
+    nmsg[s] = nm;
+    if (open_io) open_io[s] = (unsigned char)open;
+}
+
+// 0 auto, 1 fused segment kernel, 2 scan + layout + gather ("reasm_path")
+int ws_reasm_path = 0;
+
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
     unsigned int nseg, unsigned int max_frames, WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
@@ -199,6 +443,16 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     if ((reinterpret_cast<uintptr_t>(d_desc) | reinterpret_cast<uintptr_t>(d_res) | reinterpret_cast<uintptr_t>(d_msg)) & 15)
         return ws_set_msg("websocketframeBatchReassembleDevice: d_desc/d_res/d_msg not 16-B aligned");
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    // fused segment kernel for many small segments (one-shot blocks); the three-kernel
+    // path for few or large segments (its gather spreads one segment over many waves)
+    const bool fused = ws_reasm_path == 1 ||
+                       (ws_reasm_path == 0 && max_frames <= RSEG_TB && nseg >= 1024 && buflen <= (u64)nseg << 18);
+    if (fused && max_frames <= RSEG_TB) {
+        hipLaunchKernelGGL(ws_reasm_seg_kernel, dim3(nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
+                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);
+    }
     const u64 nslots = (u64)nseg * max_frames;
     const size_t piece = ws_piece_workspace_bytes(buflen, nseg, max_frames);
     const size_t rec_off = (piece + 255) & ~(size_t)255;
