@@ -25,10 +25,21 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
-KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel", 3: "ws_piece_unmask_kernel"}
-STEP_KERNELS = {3: "hipMemsetAsync(piece table) + ws_piece_walk_kernel + ws_piece_unmask_kernel + gated "
-                   "ws_walker_kernel (exits at once for ordered segments)"}
-DEFAULT_PATH = 3
+KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel", 3: "ws_piece_unmask_kernel",
+           4: "ws_segfuse_kernel"}
+STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel + gated ws_walker_kernel (exits at once "
+                   "for ordered segments)",
+                4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)"}
+DEFAULT_PATH = -1  # auto: 4 (segfuse) for >= 1024 segments of <= 17 KiB - 64 B average, max_frames <= 64; else 3
+
+
+def decode_path(path, wl):
+    """the decode variant websocketframeBatchDecodeDevice takes for this batch (ws_api.hip: decode_path)"""
+    if path == 4:
+        return 4 if wl.fps <= 64 else 3
+    if path >= 0:
+        return path
+    return 4 if wl.fps <= 64 and wl.nseg >= 1024 and wl.wire_bytes <= wl.nseg * ((17 << 10) - 64) else 3
 
 
 def pmc_traffic(kernel, algo_bytes):
@@ -527,7 +538,8 @@ def main():
     value = payload_all / elapsed / 2**30
     mean_kern = float(kern_ms.mean()) / 1e3
     achieved = wl.algo_bytes / mean_kern / 1e9
-    pmc = pmc_traffic(KERNELS[path], wl.algo_bytes)
+    kpath = decode_path(path, wl)
+    pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes)
     out = {
         "metric": "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames",
         "value": round(value, 2),
@@ -549,9 +561,9 @@ def main():
                      "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
                      "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
-                     "kernel": KERNELS[path], "algo_bytes_per_launch": wl.algo_bytes,
+                     "kernel": KERNELS[kpath], "algo_bytes_per_launch": wl.algo_bytes,
                      "timed": "HIP events around each decode call on its stream: " +
-                              STEP_KERNELS.get(path, KERNELS[path]),
+                              STEP_KERNELS.get(kpath, KERNELS[kpath]),
                      "per_kernel_ns": pmc[1].get("per_kernel_avg_ns") if pmc else None,
                      "kernel_ms_mean": round(mean_kern * 1e3, 4), "kernel_ms_min": round(float(kern_ms.min()), 4)},
         "verified": mism == 0,

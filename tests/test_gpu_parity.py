@@ -24,6 +24,15 @@ def dev():
     return torch.device("cuda:0")
 
 
+# decode variants: -1 auto (the default: 4 for many small segments, else 3), 3 the piece
+# path (scan kernel + one-shot 16 KiB piece unmask), 4 one workgroup per segment (segfuse)
+@pytest.fixture(params=[-1, 3, 4], ids=["auto", "piece", "segfuse"], autouse=True)
+def decode_path(request):
+    W.set_option("path", request.param)
+    yield request.param
+    W.set_option("path", -1)
+
+
 def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):
     """copy to device (with slack), decode, copy back. Returns (buf, desc, res)."""
     n = len(host_buf)

@@ -19,6 +19,8 @@ extern int ws_dbg_flags;
 extern size_t ws_host_chunk_bytes;
 extern int ws_piece_scan;
 extern int ws_reasm_path;
+extern int ws_reasm_cfg;
+extern int ws_segfuse_cfg;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -36,8 +38,9 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 // launch configuration (tunable for in-process A/B by bench/profiling tools)
 
 struct WsTuning {
-    int path = 3;           // 0: segment blocks (ws_segblock), 1: fused walker, 2: split walk + unmask,
-                            // 3: walk + one-shot 16 KiB pieces (ws_piece)
+    int path = -1;          // -1 auto (4 for many small segments, else 3), 0: segment blocks (ws_segblock),
+                            // 1: fused walker, 2: split walk + unmask, 3: walk + one-shot 16 KiB pieces
+                            // (ws_piece), 4: one workgroup per segment, walk + unmask fused (ws_segfuse)
     int seg_cfg = 0;        // segment-block geometry: 0 256x17, 1 512x9, 2 1024x5, 3 256x8, 4 512x4
     int split_cfg = 0;      // split unmask geometry: 0 512x9, 1 1024x5, 2 256x17, 3 512x4
     int nt = 1;             // 0 plain, 1 nontemporal loads+stores, 2 nontemporal stores only
@@ -59,6 +62,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "host_chunk_mb") && value > 0) ws_host_chunk_bytes = (size_t)value << 20;
     else if (!strcmp(name, "piece_scan")) ws_piece_scan = (int)value;
     else if (!strcmp(name, "reasm_path")) ws_reasm_path = (int)value;
+    else if (!strcmp(name, "reasm_cfg")) ws_reasm_cfg = (int)value;
+    else if (!strcmp(name, "segfuse_cfg")) ws_segfuse_cfg = (int)value;
     else return -1;
     return 0;
 }
@@ -156,10 +161,19 @@ int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
     return 0;
 }
 
+// the decode variant a call takes
+static int decode_path(const WsTuning& t, u64 span, u32 nseg, u32 max_frames) {
+    if (t.path == 4) return max_frames <= 64 ? 4 : 3;                 // segfuse holds <= 64 frames per segment
+    if (t.path >= 0) return t.path;
+    return ws_segfuse_fits(span, nseg, max_frames) ? 4 : 3;
+}
+
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     const WsTuning t = g_tune;
-    if (t.path == 3) return ws_piece_workspace_bytes(span, nseg, max_frames);
-    if (t.path == 2) return (size_t)nseg * max_frames * 4 + (size_t)nseg * 4 + 256 + 256;
+    const int path = decode_path(t, span, nseg, max_frames);
+    if (path == 3) return ws_piece_workspace_bytes(span, nseg, max_frames);
+    if (path == 4) return 0;
+    if (path == 2) return (size_t)nseg * max_frames * 4 + (size_t)nseg * 4 + 256 + 256;
     return 0;
 }
 
@@ -181,15 +195,17 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     L.stream = stream;
     L.cus = ds->cus;
     u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
-    if (t.path == 0) return ws_launch_segblock(L, t.seg_cfg, t.nt);
-    if (t.path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
+    const int path = decode_path(t, hi - lo, nseg, max_frames);
+    if (path == 0) return ws_launch_segblock(L, t.seg_cfg, t.nt);
+    if (path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
+    if (path == 4) return ws_launch_segfuse(L, t.nt);
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
     if (ws && ws_bytes < need) return ws_set_msg("websocketframe batch decode: workspace too small");
     if (!ws && need) {
         if ((rc = workspace(ds, need, L.stream))) return rc;
         ws = ds->ws;
     }
-    if (t.path == 3) {
+    if (path == 3) {
         const u32 gen = ws_next_gen();
         const u32* disorder = nullptr;
         if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder))) return rc;

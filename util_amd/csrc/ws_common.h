@@ -197,6 +197,82 @@ __device__ __forceinline__ void ws_xor_round(const u32x4 (&v)[U], gu32x4* const 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One round of the reactor loop (net_reactor.c:515-526) over a segment window staged in
+// LDS, by stride speculation, for a whole wavefront: lane k parses the header at
+// off + k*g (g = the last frame length; seeded with the length of the frame at `off`),
+// the chain is right up to the first lane whose length differs (ballot), so a run of up
+// to 64 equal frames costs one round. Window coordinates: X = segment offset + lead
+// (lead = the segment's 16-B phase); the window holds X in [W0, W0 + 16*nchunks) and
+// owns headers starting in [W0, W1) (W1 + 16 <= its end, so a header never passes it).
+// Used by the one-workgroup-per-segment kernels (ws_segfuse.hip, ws_reasm.hip).
+struct WsRound {
+    WsHdr h;        // this lane's parse
+    u64 pos;        // this lane's candidate frame offset (segment-relative)
+    u32 mm;         // first lane that does not continue the chain (64: all continue)
+    u32 code_m;     // its code: 0 continue, 1 consumed + new stride, 2 consumed + end (ret <= 0),
+                    // 3 not consumed + end, 4 header past the window (continue in the next one)
+    u32 ntake;      // lanes [0, ntake) consumed a frame (descriptor if ret != 0)
+    int ret_m, st_m;
+};
+
+__device__ __forceinline__ WsRound ws_lds_round(const u32x4* win, u64 W0, u64 W1, u64 lead, u64 sl, u64 off,
+                                                u64& g, u32 nf, u32 max_frames, u32 lane) {
+    if (g == 0 && off + lead < W1 && off < sl) {                       // stride seed
+        const u32 o = (u32)(off + lead - W0);
+        u64 h0, h1;
+        ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
+        const WsHdr h = ws_parse(h0, h1, sl - off);
+        if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
+    }
+    WsRound r;
+    r.pos = off + (u64)lane * g;
+    const bool cand = lane == 0 || g > 0;
+    const u64 X = r.pos + lead;
+    const bool inwin = X < W1;
+    const bool eval = cand && r.pos < sl && inwin;
+    const u32 o = eval ? (u32)(X - W0) : 0u;
+    u64 h0, h1;
+    ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
+    r.h = ws_parse(h0, h1, eval ? sl - r.pos : 0);
+    u32 code = 3;
+    int st = WEBSOCKET_SEG_OK;
+    if (cand) {
+        if (r.pos >= sl) code = 3;
+        else if (nf + lane >= max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
+        else if (!inwin) code = 4;
+        else if (sl - r.pos < 2) code = 3;                                 // websocketframe.c:121
+        else if (r.h.kind == WS_PARSE_INCOMPLETE) code = 3;
+        else if (r.h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
+        else if (r.h.ret <= 0) { code = 2; st = r.h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
+        else code = (u64)(u32)r.h.ret == g ? 0u : 1u;
+    }
+    const u64 stop = __ballot(code != 0);
+    r.mm = stop ? (u32)__builtin_ctzll(stop) : 64u;
+    const u32 src = r.mm < 64 ? r.mm : 63;
+    r.code_m = r.mm < 64 ? (u32)__shfl((int)code, (int)src) : 0u;
+    r.ret_m = __shfl(r.h.ret, (int)src);
+    r.st_m = __shfl(st, (int)src);
+    r.ntake = r.mm + ((r.code_m == 1 || r.code_m == 2) ? 1u : 0u);
+    return r;
+}
+
+// Advance the loop state past a round; false = no more rounds in this window (the walk
+// ended: walking = false, or the next header lies in the next window).
+__device__ __forceinline__ bool ws_round_advance(const WsRound& r, u64& off, u64& g, u32& nf, int& status,
+                                                 bool& walking) {
+    if (r.mm == 64) { nf += 64; off += 64 * g; return true; }
+    const u64 pos_m = off + (u64)r.mm * g;
+    nf += r.mm;
+    if (r.code_m == 1) { nf += 1; off = pos_m + (u32)r.ret_m; g = (u32)r.ret_m; return true; }
+    off = pos_m;
+    if (r.code_m == 4) return false;
+    if (r.code_m == 2 && r.ret_m != 0) nf += 1;                        // ret < 0 keeps its descriptor
+    status = r.st_m;
+    walking = false;
+    return false;
+}
+
 // host side
 int ws_set_err(const char* what, hipError_t e);
 int ws_set_msg(const char* msg);
@@ -238,3 +314,5 @@ int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, cons
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 int ws_launch_split(const WsLaunch& L, int variant, int nt, u32* keys, u32* nwork);
 int ws_launch_segblock(const WsLaunch& L, int cfg, int nt);
+int ws_launch_segfuse(const WsLaunch& L, int nt);
+bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
 // ---------------------------------------------------------------------------------------------
 // Fused path: ONE workgroup per rx segment, the whole decode + reassembly of the segment
 // in one kernel. The segment's wire bytes stream through LDS in windows (one window for
-// segments up to 19 KiB: cfg5's 16.5 KiB messages are one-shot blocks — load once,
+// segments up to 17 KiB: cfg5's 16.5 KiB messages are one-shot blocks — load once,
 // store once, exit, the pattern that reaches the part's streaming ceiling):
 //   1. LDS-DMA (global_load_lds_dwordx4): every wave issues its 1 KiB slices of the
 //      window at once, clamped to the segment's readable bytes (segment +
@@ -210,27 +210,28 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
 // Each wire byte is read from HBM once (+ 1 KiB of look-ahead per extra window), each
 // body byte written once.
 #define RSEG_T 256
-#define RSEG_L 20                                  // LDS-DMA wave instructions per window (1 KiB each)
-#define RSEG_C ((RSEG_L - 1) * 64)                 // chunks owned per window: 19 KiB (+1 KiB look-ahead)
+// window = L LDS-DMA wave instructions of 1 KiB: (L-1) KiB owned + 1 KiB look-ahead;
+// L = 18 is ~20 KB of LDS: 8 workgroups (32 waves) per CU ("reasm_cfg" A/B: ws_reasm_cfg)
 #define RSEG_TB 64                                 // body table entries = max max_frames of this path
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-struct BodyL {           // body table entry (LDS)
-    u64 x0;              // first payload byte, window coordinates (segment offset + lead)
-    u64 dst;             // first body byte, region-relative
-    u64 len;
-    u32 key;             // key rotated to the absolute output phase (0 for unmasked frames)
-    u32 pad;
+struct BodyL {           // body table entry (LDS; its key, rotated to the absolute output phase
+    u64 x0;              // (0 for unmasked frames), in a separate array to keep LDS at 20 KB)
+    u64 dst;             // first payload byte in window coordinates (segment offset + lead),
+    u64 len;             // first body byte region-relative, body length
 };
 
-__global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
+template <int RSEG_L, int MINW>
+__global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void ws_reasm_seg_kernel(
     const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
     const u64* __restrict__ seg_len, WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     unsigned char* __restrict__ out, const u64* __restrict__ out_off, WebsocketMsgDesc_t* __restrict__ msg,
     u32* __restrict__ nmsg, unsigned char* __restrict__ open_io) {
+    constexpr u32 RSEG_C = (RSEG_L - 1) * 64;         // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[RSEG_L * 64];
     __shared__ BodyL tab[RSEG_TB];
+    __shared__ u32 tkey[RSEG_TB];
     __shared__ u64 sh_next;                        // next window's first chunk, ~0 = done
     __shared__ u32 sh_blo, sh_bhi;                 // bodies with bytes in this window [blo, bhi], blo > bhi: none
     const u32 s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -267,44 +268,10 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
         // ---- 2. wave 0: headers starting in [W0, W1)
         if (w0) {
             while (walking) {
-                // stride seed: the length of the frame at `off` (speculation verified below)
-                if (g == 0 && off + lead < W1 && off < sl) {
-                    const u32 o = (u32)(off + lead - W0);
-                    u64 h0, h1;
-                    ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
-                    const WsHdr h = ws_parse(h0, h1, sl - off);
-                    if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
-                }
-                const u64 pos = off + (u64)lane * g;
-                const bool cand = lane == 0 || g > 0;
-                const u64 X = pos + lead;
-                const bool inwin = X < W1;
-                const bool eval = cand && pos < sl && inwin;
-                const u32 o = eval ? (u32)(X - W0) : 0u;
-                u64 h0, h1;
-                ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
-                const WsHdr h = ws_parse(h0, h1, eval ? sl - pos : 0);
-                // 0 consumed, chain continues  1 consumed, new stride  2 consumed, walk ends (ret <= 0)
-                // 3 not consumed, walk ends    4 header past this window: continue in the next one
-                u32 code = 3;
-                int st = WEBSOCKET_SEG_OK;
-                if (cand) {
-                    if (pos >= sl) code = 3;
-                    else if (nf + lane >= max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
-                    else if (!inwin) code = 4;
-                    else if (sl - pos < 2) code = 3;                          // websocketframe.c:121
-                    else if (h.kind == WS_PARSE_INCOMPLETE) code = 3;
-                    else if (h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
-                    else if (h.ret <= 0) { code = 2; st = h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
-                    else code = (u64)(u32)h.ret == g ? 0u : 1u;
-                }
-                const u64 stop = __ballot(code != 0);
-                const u32 mm = stop ? (u32)__builtin_ctzll(stop) : 64u;
-                const u32 src = mm < 64 ? mm : 63;
-                const u32 code_m = mm < 64 ? (u32)__shfl((int)code, (int)src) : 0u;
-                const int ret_m = __shfl(h.ret, (int)src);
-                const int st_m = __shfl(st, (int)src);
-                const u32 ntake = mm + ((code_m == 1 || code_m == 2) ? 1u : 0u);
+                const WsRound r = ws_lds_round(win, W0, W1, lead, sl, off, g, nf, max_frames, lane);
+                const WsHdr& h = r.h;
+                const u64 pos = r.pos, X = pos + lead;
+                const u32 mm = r.mm, code_m = r.code_m, ntake = r.ntake;
                 if (lane < ntake && h.ret != 0) ws_store_desc(desc + base + nf + lane, so + pos, h);
                 // bodies: consumed frames with ret > 0 (the a6 delivery rule), each at the
                 // running sum of the bodies before it; none after an overflow
@@ -326,8 +293,8 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
                     if (lane < ntb) {
                         BodyL b;
                         b.x0 = X + h.hdr; b.dst = qs; b.len = len;
-                        b.key = h.masked ? rotl32(h.key, 8u * (u32)((obase + qs) & 3)) : 0u; b.pad = 0;
                         tab[nb + lane] = b;
+                        tkey[nb + lane] = h.masked ? rotl32(h.key, 8u * (u32)((obase + qs) & 3)) : 0u;
                     }
                     // messages closed by FIN frames among the taken bodies (body index == frame index)
                     const bool fin = lane < ntb && (h.b0 >> 7);
@@ -358,16 +325,7 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
                     q += ntb ? tot : 0;
                     nb += ntb;
                 }
-                // advance the reactor loop
-                if (mm == 64) { nf += 64; off += 64 * g; continue; }
-                const u64 pos_m = off + (u64)mm * g;
-                nf += mm;
-                if (code_m == 1) { nf += 1; off = pos_m + (u32)ret_m; g = (u32)ret_m; continue; }
-                off = pos_m;
-                if (code_m == 4) break;                                      // next header: next window
-                if (code_m == 2 && ret_m != 0) nf += 1;                      // ret < 0 keeps its descriptor
-                status = st_m;
-                walking = false;
+                if (!ws_round_advance(r, off, g, nf, status, walking)) break;
             }
             // bodies with bytes in [W0, W1), and where the next window starts
             const BodyL t = tab[lane];
@@ -384,6 +342,7 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
         const u32 bhi = sh_bhi;
         for (u32 bi = sh_blo + wv; bi <= bhi; bi += RSEG_T / 64) {
             const BodyL b = tab[bi];
+            const u32 key = tkey[bi];
             if (!b.len) continue;
             const u64 xa = b.x0 > W0 ? b.x0 : W0, xe = b.x0 + b.len < W1 ? b.x0 + b.len : W1;
             const u64 da = obase + b.dst + (xa - b.x0), de = da + (xe - xa);   // absolute output range
@@ -397,8 +356,8 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
                     u64 h0, h1;
                     ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
                     u32x4 w;
-                    w.x = (u32)h0 ^ b.key; w.y = (u32)(h0 >> 32) ^ b.key;
-                    w.z = (u32)h1 ^ b.key; w.w = (u32)(h1 >> 32) ^ b.key;
+                    w.x = (u32)h0 ^ key; w.y = (u32)(h0 >> 32) ^ key;
+                    w.z = (u32)h1 ^ key; w.w = (u32)(h1 >> 32) ^ key;
                     st16<1>(w, reinterpret_cast<gu32x4*>(A + ((u64)c << 4)));
                 }
             }
@@ -408,7 +367,7 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
             if (lane < 16) { y = da + lane; act = y < (A < de ? A : de); }
             else if (lane < 32) { y = (A > B ? A : B) + (lane - 16); act = y < de; }
             if (act) {
-                const u32 kb = (b.key >> (8u * (u32)(y & 3))) & 0xFFu;
+                const u32 kb = (key >> (8u * (u32)(y & 3))) & 0xFFu;
                 *reinterpret_cast<gu8*>(y) = (unsigned char)(wb[xa - W0 + (y - da)] ^ kb);
             }
         }
@@ -431,6 +390,9 @@ __global__ __launch_bounds__(RSEG_T) void ws_reasm_seg_kernel(
 
 // 0 auto, 1 fused segment kernel, 2 scan + layout + gather ("reasm_path")
 int ws_reasm_path = 0;
+// fused kernel geometry ("reasm_cfg"): 0 17 KiB windows + 8 waves/SIMD (SGPR spills: slower),
+// 1 17 KiB windows at the compiler's occupancy (7 waves/SIMD, default), 2 19 KiB windows
+int ws_reasm_cfg = 1;
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
@@ -448,7 +410,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     const bool fused = ws_reasm_path == 1 ||
                        (ws_reasm_path == 0 && max_frames <= RSEG_TB && nseg >= 1024 && buflen <= (u64)nseg << 18);
     if (fused && max_frames <= RSEG_TB) {
-        hipLaunchKernelGGL(ws_reasm_seg_kernel, dim3(nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
+        auto k = ws_reasm_cfg == 1 ? ws_reasm_seg_kernel<18, 1>
+                                   : (ws_reasm_cfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
+        hipLaunchKernelGGL(k, dim3(nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
                            d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);
