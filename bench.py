@@ -245,6 +245,7 @@ def run_encode(args, dev, world, rank):
     mism = int(D.allreduce([wl.verify()], device=dev)[0])
     mean_kern = float(kern_ms.mean()) / 1e3
     achieved = wl.algo_bytes / mean_kern / 1e9
+    pmc = pmc_traffic("ws_enc_copy_kernel", wl.algo_bytes)
     out = {
         "metric": "WebSocket client encode+mask GiB/s (device-resident), %d x %d B frames" % (wl.nframes, wl.plen),
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
@@ -255,17 +256,64 @@ def run_encode(args, dev, world, rank):
                    "frames_per_gpu": wl.nframes, "wire_bytes_per_gpu": wl.wire_bytes,
                    "payload_bytes_per_gpu": wl.payload_bytes},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
+                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
                      "kernel": "ws_enc_copy_kernel", "algo_bytes_per_launch": wl.algo_bytes,
-                     "timed": "HIP events around each encode call: hipcub scan + ws_enc_ptr_kernel + "
-                              "ws_enc_copy_kernel",
+                     "timed": "HIP events around each encode call on its stream: hipcub scan + ws_enc_ptr_kernel + "
+                              "ws_enc_copy_kernel + ws_enc_edge_kernel",
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu_encode_baseline(wl, min(args.cpu_threads, os.cpu_count() or 1))
+        if rank == 0 and world == 1 and not args.no_cpu else None,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     return mism
+
+
+def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0):
+    """the reference's header encoder + client masking loop (oracle/ref_loop.c:ref_encode_frames)
+    on host cores, over the first `nframes` frames of the workload"""
+    ref = os.path.join(REPO, "oracle", "_ref", "libwsref_loop.so")
+    if not os.path.exists(ref):
+        return None
+    lib = C.CDLL(ref)
+    fn = lib.ref_encode_frames
+    fn.restype = C.c_ulonglong
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint, C.c_void_p]
+    n = min(nframes, wl.nframes)
+    fr = wl.frames[:n * wl.W.ENC_DTYPE.itemsize].cpu().numpy().view(wl.W.ENC_DTYPE)
+    src = wl.src[:n * wl.plen].cpu().numpy()
+    so = np.ascontiguousarray(fr["src_off"])
+    ln = np.ascontiguousarray(fr["len"])
+    key = np.ascontiguousarray(fr["mask_key"])
+    bounds = np.linspace(0, n, threads + 1).astype(int)
+    dsts = [np.empty(int(ln[bounds[i]:bounds[i + 1]].sum()) + (bounds[i + 1] - bounds[i]) * 14 + 16, np.uint8)
+            for i in range(threads)]
+
+    def run(i, passes):
+        a, b = bounds[i], bounds[i + 1]
+        for _ in range(passes):
+            fn(src.ctypes.data, so[a:].ctypes.data, ln[a:].ctypes.data, key[a:].ctypes.data, b - a, dsts[i].ctypes.data)
+
+    def timed(nthreads, passes):
+        ths = [threading.Thread(target=run, args=(i, passes)) for i in range(nthreads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0
+    payload = int(ln.sum())
+    t1 = timed(1, 1) * threads                     # thread 0 does 1/threads of the frames
+    passes = max(2, int(min_seconds / max(1e-6, t1 / threads)))
+    tn = timed(threads, passes)
+    return {"value": round(payload * passes / tn / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_thread_gibs": round(payload / t1 / 2**30, 3), "cpu_seconds": round(tn * threads + t1, 2),
+            "sample": "%d frames (%.1f MiB payload) of the same workload, %d passes x %d threads, reference "
+                      "websocketframeEncode headers + client masking loop (restated)" %
+                      (n, payload / 2**20, passes, threads)}
 
 
 def reasm_fused(wl):
@@ -333,7 +381,7 @@ def run_reasm(args, dev, world, rank):
     kname = "ws_reasm_seg_kernel" if fused else "ws_reasm_gather_kernel"
     pmc = pmc_traffic(kname, algo)
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wl.host_sample(262144), min(args.cpu_threads, os.cpu_count() or 1), op="reasm",
                            frames_per_segment=wl.fps)
     out_json = {

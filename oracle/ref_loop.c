@@ -109,3 +109,40 @@ unsigned long long ref_reassemble_segments(unsigned char* buf, const unsigned lo
     *messages = nm;
     return sum;
 }
+
+/*
+ * Encode baseline (client side): every frame's header from the
+ * reference's websocketframeEncodeHeadLength/websocketframeEncode
+ * (src/crt/protocol/websocketframe.c:167-202), then — as a client must (RFC 6455 §5.3),
+ * which the reference encoder leaves to its caller — the MASK bit, the 4 key bytes and
+ * the payload copied with the same per-byte XOR loop the reference uses to unmask
+ * (websocketframe.c:153-158). Frames are laid out back to back in dst. Returns bytes
+ * written.
+ */
+unsigned int websocketframeEncodeHeadLength(unsigned long long datalen);
+void websocketframeEncode(void* headbuf, int is_fin, int prev_is_fin, int type, unsigned long long datalen);
+
+__attribute__((visibility("default")))
+unsigned long long ref_encode_frames(const unsigned char* src, const unsigned long long* src_off,
+                                     const unsigned long long* len, const unsigned int* key, unsigned int n,
+                                     unsigned char* dst) {
+    unsigned long long o = 0;
+    unsigned int i;
+    for (i = 0; i < n; ++i) {
+        unsigned int hl = websocketframeEncodeHeadLength(len[i]);
+        unsigned char* h = dst + o;
+        const unsigned char* p = src + src_off[i];
+        unsigned char* d;
+        unsigned char k[4];
+        unsigned long long j;
+        websocketframeEncode(h, 1, 1, 2, len[i]);
+        h[1] |= 0x80;
+        k[0] = (unsigned char)key[i]; k[1] = (unsigned char)(key[i] >> 8);
+        k[2] = (unsigned char)(key[i] >> 16); k[3] = (unsigned char)(key[i] >> 24);
+        memcpy(h + hl, k, 4);
+        d = h + hl + 4;
+        for (j = 0; j < len[i]; ++j) d[j] = p[j] ^ k[j % 4];
+        o += hl + 4 + len[i];
+    }
+    return o;
+}

@@ -21,6 +21,8 @@ extern int ws_piece_scan;
 extern int ws_reasm_path;
 extern int ws_reasm_cfg;
 extern int ws_segfuse_cfg;
+extern int ws_encode_side;
+extern int ws_piece_whole;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -64,6 +66,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "reasm_path")) ws_reasm_path = (int)value;
     else if (!strcmp(name, "reasm_cfg")) ws_reasm_cfg = (int)value;
     else if (!strcmp(name, "segfuse_cfg")) ws_segfuse_cfg = (int)value;
+    else if (!strcmp(name, "encode_side")) ws_encode_side = (int)value;
+    else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else return -1;
     return 0;
 }

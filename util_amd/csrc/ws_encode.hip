@@ -15,6 +15,8 @@
 // E4 one thread per frame assembles the other chunks whose first byte lies in its wire
 //    extent (header bytes, frame edges; header bytes computed, payload bytes loaded)
 //    and stores each with one 16-B store. Every output chunk is written exactly once.
+//    E4 touches only chunks E3 skips; option "encode_side" runs it on a side stream
+//    concurrently with E2+E3 (measured slower on MI355X, so off by default).
 #include <hipcub/hipcub.hpp>
 
 #include "ws_common.h"
@@ -182,6 +184,81 @@ __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* _
     const u64 out_lo = lead0, out_hi = lead0 + total;
     const EncFrame e = enc_load(f, wire_off, i);
     const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
+    // Fast path (payload >= 32 B, nothing clipped): the head chunk [X0, +16) = header +
+    // payload bytes [0, 16) (only if the header reaches past X0), the tail chunk [XT, +16)
+    // = payload bytes [len-16, len) + the next frame's header (+ its payload bytes [0, 16),
+    // which must then be >= 16 B long): the next record and the 16-B source windows a
+    // chunk needs are loaded together, one round trip after this frame's record.
+    {
+        const u64 X0 = (o + 15) & ~15ull, XT = d1 & ~15ull;
+        const bool nxt = i + 1 < n, head = X0 < d0, tail = (d1 & 15) != 0;
+        if (e.len >= 32 && (i > 0 || (o & 15) == 0) && o >= out_lo && XT + 16 <= out_hi) {
+            EncFrame nx = {};
+            u32x4 wh = {0, 0, 0, 0}, wt = {0, 0, 0, 0}, wn = {0, 0, 0, 0};
+            if (tail && nxt) nx = enc_load(f, wire_off, i + 1);
+            if (head) wh = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src));
+            if (tail)
+                wt = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src + e.len - 16));
+            const u64 dn0 = d1 + nx.hl;                                      // next payload start
+            const bool npay = tail && nxt && dn0 < XT + 16;                  // next payload enters the tail chunk
+            if (npay && nx.len < 16) goto generic;
+            if (npay) wn = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + nx.src));
+            const u32 kh = e.masked ? e.key : 0u, kn = nx.masked ? nx.key : 0u;
+            if (head) {                                                      // head chunk holds header bytes
+                u32x4 w = {0, 0, 0, 0};
+                for (u32 q = 0; q < 16; ++q) {
+                    const u64 y = X0 + q;
+                    u32 v;
+                    if (y < d0) {
+                        v = enc_header_byte(e, (u32)(y - o));
+                    } else {
+                        const u32 pi = (u32)(y - d0);
+                        const u32 wq = pi < 4 ? wh.x : (pi < 8 ? wh.y : (pi < 12 ? wh.z : wh.w));
+                        v = ((wq >> (8u * (pi & 3))) ^ (kh >> (8u * (pi & 3)))) & 0xFFu;
+                    }
+                    put_byte(w, q, v);
+                }
+                base[X0 >> 4] = w;
+            }
+            if (tail) {                                                      // tail chunk: this + next frame
+                u32x4 w = {0, 0, 0, 0};
+                u32 cov = 0;
+                for (u32 q = 0; q < 16; ++q) {
+                    const u64 y = XT + q;
+                    u32 v;
+                    if (y < d1) {
+                        const u64 pi = y - d0;
+                        const u32 t = (u32)(pi - (e.len - 16));
+                        const u32 wq = t < 4 ? wt.x : (t < 8 ? wt.y : (t < 12 ? wt.z : wt.w));
+                        v = ((wq >> (8u * (t & 3))) ^ (kh >> (8u * (u32)(pi & 3)))) & 0xFFu;
+                    } else if (!nxt) {
+                        continue;                                            // past the batch
+                    } else if (y < dn0) {
+                        v = enc_header_byte(nx, (u32)(y - d1));
+                    } else {
+                        const u32 pi = (u32)(y - dn0);
+                        const u32 wq = pi < 4 ? wn.x : (pi < 8 ? wn.y : (pi < 12 ? wn.z : wn.w));
+                        v = ((wq >> (8u * (pi & 3))) ^ (kn >> (8u * (pi & 3)))) & 0xFFu;
+                    }
+                    put_byte(w, q, v);
+                    cov |= 1u << q;
+                }
+                gu32x4* const pc = base + (XT >> 4);
+                if (cov == 0xFFFFu) {
+                    *pc = w;
+                } else {
+                    gu8* const pb = reinterpret_cast<gu8*>(pc);
+                    for (u32 q = 0; q < 16; ++q) {
+                        if (!((cov >> q) & 1u)) continue;
+                        const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
+                        pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
+                    }
+                }
+            }
+            return;
+        }
+    }
+generic:
     u64 X = i ? ((o + 15) & ~15ull) : (o & ~15ull);                           // first chunk start owned
     const u64 lim = d1 < out_hi ? d1 : out_hi;                               // interior chunks end here
     for (; X < d1 && X < out_hi; X += 16) {
@@ -239,6 +316,31 @@ __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* _
 
 int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out);
 
+// per-device side stream + fork/join events for E4 (created on first use)
+#define ENC_MAX_DEV 64
+struct EncSide {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static EncSide g_side[ENC_MAX_DEV];
+
+static int enc_side(EncSide** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return ws_set_err("hipGetDevice", e);
+    if (dev < 0 || dev >= ENC_MAX_DEV) return ws_set_err("device index", hipErrorInvalidDevice);
+    EncSide& S = g_side[dev];
+    if (!S.s) {
+        if ((e = hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking)) != hipSuccess) return ws_set_err("hipStreamCreate", e);
+        if ((e = hipEventCreateWithFlags(&S.fork, hipEventDisableTiming)) != hipSuccess) return ws_set_err("hipEventCreate", e);
+        if ((e = hipEventCreateWithFlags(&S.join, hipEventDisableTiming)) != hipSuccess) return ws_set_err("hipEventCreate", e);
+    }
+    *out = &S;
+    return 0;
+}
+int ws_encode_side = 0;   // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
+                          // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
+
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,
                                                                   const WebsocketEncodeDesc_t* d_frames,
                                                                   unsigned int nframes, unsigned char* d_dst,
@@ -263,6 +365,16 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
         return ws_set_err("hipcub scan", e);
     u32* ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
+    EncSide* S = nullptr;
+    if (ws_encode_side) {
+        if ((rc = enc_side(&S))) return rc;
+        if ((e = hipEventRecord(S->fork, st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+        if ((e = hipStreamWaitEvent(S->s, S->fork, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
+        hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, S->s, d_src, d_frames,
+                           nframes, d_wire_off, d_dst, (u64)dst_capacity);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
+        if ((e = hipEventRecord(S->join, S->s)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+    }
     hipLaunchKernelGGL(ws_enc_ptr_kernel, dim3((nframes + 1 + 255) / 256), dim3(256), 0, st, d_frames, nframes,
                        d_wire_off, ptr, lead0, npieces);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
@@ -270,6 +382,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         hipLaunchKernelGGL((ws_enc_copy_kernel<1>), dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
                            d_wire_off, ptr, d_dst, (u64)dst_capacity);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
+    }
+    if (S) {
+        if ((e = hipStreamWaitEvent(st, S->join, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
+        return 0;
     }
     hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, d_src, d_frames, nframes,
                        d_wire_off, d_dst, (u64)dst_capacity);

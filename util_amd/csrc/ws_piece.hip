@@ -219,7 +219,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     }
 }
 
-template <int NT>
+template <int NT, u32 WHOLE>
 __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
                                                                   const u64* __restrict__ seg_len, u32 nseg,
@@ -254,8 +254,18 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     u32 s = ok && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
+    u32 whole = 0;   // bit u: chunk u lies inside one segment whose frames touch it — stored whole (bytes the
+                     // decode does not change are written back unchanged: full-line writes, no read-modify-write)
     while (s < nseg) {
         const u32 cnt = nwork[s];
+        {
+            const u64 sa = seg_off[s] + lead0, sb = sa + seg_len[s];        // origin-relative segment bytes
+#pragma unroll
+            for (int u = 0; u < PIECE_U; ++u) {
+                const u64 x = r0 + (u64)(u * 1024 + xl);
+                whole |= (x >= sa && x + 16 <= sb) ? (1u << u) : 0u;
+            }
+        }
         if (k < cnt) {
             const u32 j = k + lane;
             const bool valid = j < cnt;
@@ -304,7 +314,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         u32x4 w = v[u];
         w.x ^= m[u][0]; w.y ^= m[u][1]; w.z ^= m[u][2]; w.w ^= m[u][3];
-        if (cov[u] == 0xFFFFu) {
+        if (cov[u] == 0xFFFFu || ((whole >> u) & WHOLE)) {
             st16<NT>(w, base + c);
         } else {
             gu8* const pb = reinterpret_cast<gu8*>(base + c);
@@ -370,16 +380,14 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 }
 
 // K2 alone over the pieces of a scanned batch
+int ws_piece_whole = 1;   // "piece_whole": 1 store in-segment edge chunks whole (default), 0 exact bytes only
+
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
     if (!P.npieces) return 0;
-    if (nt == 1)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1>), dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                           L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
-                           P.c_lo, P.c_hi);
-    else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<0>), dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf,
-                           L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
-                           P.c_lo, P.c_hi);
+    auto k = nt == 1 ? (ws_piece_whole ? ws_piece_unmask_kernel<1, 1> : ws_piece_unmask_kernel<1, 0>)
+                     : (ws_piece_whole ? ws_piece_unmask_kernel<0, 1> : ws_piece_unmask_kernel<0, 0>);
+    hipLaunchKernelGGL(k, dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
+                       L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
 }
