@@ -35,6 +35,9 @@ DEFAULT_PATH = -1  # auto: 4 (segfuse) for >= 1024 segments of <= 17 KiB - 64 B 
 
 def decode_path(path, wl):
     """the decode variant websocketframeBatchDecodeDevice takes for this batch (ws_api.hip: decode_path)"""
+    opt = dict(kv.split("=") for kv in filter(None, os.environ.get("WSFRAME_AMD_OPTIONS", "").split(",")))
+    if "path" in opt:
+        path = int(opt["path"])
     if path == 4:
         return 4 if wl.fps <= 64 else 3
     if path >= 0:
@@ -518,6 +521,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
+    ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
     ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm"],
                     help="decode (the headline), client-side encode + mask of the same frames, or fused "
                          "decode + message reassembly (use with --config cfg5)")
@@ -543,7 +547,7 @@ def main():
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)
 
-    wl = Workload.make(args.config, dev, seed_offset=rank)
+    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank)
     torch.cuda.synchronize()
     sample = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -254,8 +254,12 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     u32 s = ok && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
-    u32 whole = 0;   // bit u: chunk u lies inside one segment whose frames touch it — stored whole (bytes the
-                     // decode does not change are written back unchanged: full-line writes, no read-modify-write)
+    // segcov[u]: bytes of chunk u inside the segments visited here. A chunk wholly inside
+    // segments is stored whole (bytes the decode does not change are written back
+    // unchanged: one 16-B store instead of byte stores); others get exact byte stores.
+    u32 segcov[PIECE_U];
+#pragma unroll
+    for (int u = 0; u < PIECE_U; ++u) segcov[u] = 0;
     while (s < nseg) {
         const u32 cnt = nwork[s];
         {
@@ -263,7 +267,9 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
 #pragma unroll
             for (int u = 0; u < PIECE_U; ++u) {
                 const u64 x = r0 + (u64)(u * 1024 + xl);
-                whole |= (x >= sa && x + 16 <= sb) ? (1u << u) : 0u;
+                const u32 lo = sa > x ? (sa - x < 16 ? (u32)(sa - x) : 16u) : 0u;
+                const u32 hi = sb > x ? (sb - x < 16 ? (u32)(sb - x) : 16u) : 0u;
+                if (hi > lo) segcov[u] |= (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
             }
         }
         if (k < cnt) {
@@ -314,7 +320,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         u32x4 w = v[u];
         w.x ^= m[u][0]; w.y ^= m[u][1]; w.z ^= m[u][2]; w.w ^= m[u][3];
-        if (cov[u] == 0xFFFFu || ((whole >> u) & WHOLE)) {
+        if (cov[u] == 0xFFFFu || (WHOLE && segcov[u] == 0xFFFFu)) {
             st16<NT>(w, base + c);
         } else {
             gu8* const pb = reinterpret_cast<gu8*>(base + c);
