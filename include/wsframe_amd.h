@@ -115,7 +115,9 @@ typedef struct WebsocketSegResult_t {
  * `hip_stream` (hipStream_t, NULL = default stream).
  *   d_buf          batch buffer (device); payloads are unmasked in place
  *   buflen         every segment lies in [0, buflen) of d_buf; d_buf[0, buflen + WEBSOCKET_BATCH_PAD)
- *                  must be readable (the kernels read, never write, bytes outside segments)
+ *                  must be readable (the kernels read, never write, bytes outside segments;
+ *                  bytes inside a segment that the decode does not change may be written
+ *                  back with their own value — whole 16-B stores)
  *   d_seg_off/len  nseg segments [off, off+len) of d_buf (device arrays); must not overlap;
  *                  ascending order is fastest (any order is decoded correctly)
  *   max_frames     descriptor capacity per segment (>= 1)
@@ -165,10 +167,13 @@ WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, un
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
- * configuration): "path" (0 segment blocks, 1 walker, 2 split), "host_chunk_mb", "dyn" (1 dynamic segment dequeue / 0 static), "unroll"
- * (2|4|8 x 16-B chunks per lane per batch), "nt" (0 plain / 1 nontemporal
- * loads+stores / 2 nontemporal stores), "blocks_per_cu" (0 = resident limit).
- * Returns 0, or -1 for an unknown name. Not thread-safe against concurrent calls. */
+ * configuration): "path" (-1 auto, 0 segment blocks, 1 walker, 2 split, 3 piece,
+ * 4 segfuse), "piece_scan", "piece_whole", "segfuse_cfg", "reasm_path" (0 auto,
+ * 1 fused, 2 three-kernel), "reasm_cfg", "encode_side", "host_chunk_mb", "dyn"
+ * (1 dynamic segment dequeue / 0 static), "unroll" (2|4|8 x 16-B chunks per lane per
+ * batch), "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
+ * "blocks_per_cu" (0 = resident limit). Returns 0, or -1 for an unknown name. Not
+ * thread-safe against concurrent calls. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
 /* ---- Part 2b: fused decode + fragmented-message reassembly -- */
