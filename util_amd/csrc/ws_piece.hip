@@ -219,8 +219,8 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     }
 }
 
-template <int NT, u32 WHOLE>
-__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
+template <int NT, u32 WHOLE, int OCC>
+__global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
                                                                   const u64* __restrict__ seg_len, u32 nseg,
                                                                   u32 max_frames, const u32x4* __restrict__ items,
@@ -254,22 +254,32 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     u32 s = ok && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
-    // segcov[u]: bytes of chunk u inside the segments visited here. A chunk wholly inside
-    // segments is stored whole (bytes the decode does not change are written back
-    // unchanged: one 16-B store instead of byte stores); others get exact byte stores.
+    // Chunks that hold payload bytes and lie wholly inside segments are stored whole
+    // (bytes the decode does not change are written back unchanged: one 16-B store
+    // instead of byte stores); others get exact byte stores. WHOLE 1: a bit per chunk
+    // inside ONE visited segment (72 VGPRs); WHOLE 2: byte coverage by the visited
+    // segments, so chunks spanning two adjacent segments count too (80 VGPRs).
+    u32 whole = 0;
     u32 segcov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) segcov[u] = 0;
     while (s < nseg) {
         const u32 cnt = nwork[s];
-        {
-            const u64 sa = seg_off[s] + lead0, sb = sa + seg_len[s];        // origin-relative segment bytes
+        if (WHOLE) {
+            // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
+            const long long sa = (long long)(seg_off[s] + lead0 - r0), sb = sa + (long long)seg_len[s];
+            const int SA = (int)(sa < -16 ? -16 : (sa > RW + 16 ? RW + 16 : sa));
+            const int SB = (int)(sb < -16 ? -16 : (sb > RW + 16 ? RW + 16 : sb));
 #pragma unroll
             for (int u = 0; u < PIECE_U; ++u) {
-                const u64 x = r0 + (u64)(u * 1024 + xl);
-                const u32 lo = sa > x ? (sa - x < 16 ? (u32)(sa - x) : 16u) : 0u;
-                const u32 hi = sb > x ? (sb - x < 16 ? (u32)(sb - x) : 16u) : 0u;
-                if (hi > lo) segcov[u] |= (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+                const int x = u * 1024 + xl;
+                if constexpr (WHOLE == 1) {
+                    whole |= (x >= SA && x + 16 <= SB) ? (1u << u) : 0u;
+                } else {
+                    const int lo = SA > x ? (SA - x < 16 ? SA - x : 16) : 0;
+                    const int hi = SB > x ? (SB - x < 16 ? SB - x : 16) : 0;
+                    if (hi > lo) segcov[u] |= (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+                }
             }
         }
         if (k < cnt) {
@@ -320,7 +330,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         u32x4 w = v[u];
         w.x ^= m[u][0]; w.y ^= m[u][1]; w.z ^= m[u][2]; w.w ^= m[u][3];
-        if (cov[u] == 0xFFFFu || (WHOLE && segcov[u] == 0xFFFFu)) {
+        if (cov[u] == 0xFFFFu || (WHOLE == 1 && ((whole >> u) & 1u)) || (WHOLE == 2 && segcov[u] == 0xFFFFu)) {
             st16<NT>(w, base + c);
         } else {
             gu8* const pb = reinterpret_cast<gu8*>(base + c);
@@ -386,12 +396,20 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 }
 
 // K2 alone over the pieces of a scanned batch
-int ws_piece_whole = 1;   // "piece_whole": 1 store in-segment edge chunks whole (default), 0 exact bytes only
+int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
+                          // one segment, 0 exact bytes only
+int ws_piece_occ = 0;     // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
 
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
     if (!P.npieces) return 0;
-    auto k = nt == 1 ? (ws_piece_whole ? ws_piece_unmask_kernel<1, 1> : ws_piece_unmask_kernel<1, 0>)
-                     : (ws_piece_whole ? ws_piece_unmask_kernel<0, 1> : ws_piece_unmask_kernel<0, 0>);
+    auto k = nt == 1 ? (ws_piece_whole == 2 ? ws_piece_unmask_kernel<1, 2, 1>
+                                            : (ws_piece_whole == 1 ? ws_piece_unmask_kernel<1, 1, 1>
+                                                                   : ws_piece_unmask_kernel<1, 0, 1>))
+                     : (ws_piece_whole == 2 ? ws_piece_unmask_kernel<0, 2, 1>
+                                            : (ws_piece_whole == 1 ? ws_piece_unmask_kernel<0, 1, 1>
+                                                                   : ws_piece_unmask_kernel<0, 0, 1>));
+    if (ws_piece_occ == 7 || ws_piece_occ == 8)           // forced occupancy: spills, measured slower
+        k = ws_piece_occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
     hipLaunchKernelGGL(k, dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                        L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi);
     const hipError_t e = hipGetLastError();
