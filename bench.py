@@ -97,6 +97,8 @@ class Workload:
         "cfg3": (1 << 20, 1, 0, 0, 3, 16),
         "cfg4": (1 << 20, 0, 65536, 0, 4, 16),   # per GPU: 8M x 64 KiB over 8 GPUs
         "cfg5": (1 << 22, 0, 1024, 2, 5, 16),    # 256K messages x 16 fragments
+        # not a BASELINE config: cfg5 with 1000-B fragments (bodies off the 16-B grid)
+        "cfg5u": (1 << 22, 0, 1000, 2, 6, 16),
     }
     DESCRIPTION = {
         "cfg1": "16 masked text frames x 125 B",
@@ -104,6 +106,7 @@ class Workload:
         "cfg3": "1M frames, payload uniform from {125 B, 1500 B, 64 KiB}, 16-frame rx segments",
         "cfg4": "1M masked binary frames x 64 KiB per GPU (8M over 8 GPUs)",
         "cfg5": "256K messages x 16 continuation frames x 1 KiB (16-frame segments = messages)",
+        "cfg5u": "256K messages x 16 continuation frames x 1000 B (bodies off the 16-B grid)",
     }
 
     @classmethod

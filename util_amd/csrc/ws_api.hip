@@ -24,6 +24,7 @@ extern int ws_segfuse_cfg;
 extern int ws_encode_side;
 extern int ws_piece_whole;
 extern int ws_piece_occ;
+extern int ws_reasm_merge;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -70,6 +71,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "encode_side")) ws_encode_side = (int)value;
     else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
+    else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else return -1;
     return 0;
 }

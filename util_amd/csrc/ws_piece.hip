@@ -126,7 +126,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
                                                                 u32 gen, u64 pbase, u64 lo, u64 hi) {
-    static_assert(G == 16 || G == 32 || G == 64, "group size");
+    static_assert(G == 8 || G == 16 || G == 32 || G == 64, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
     const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / G;
@@ -360,7 +360,7 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 
 // Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *disorder_out = the word a gated
 // fallback walker compares with `gen`.
-int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3: 64/32/16 lanes per segment
+int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
 
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out) {
@@ -377,10 +377,11 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     P.nwork = reinterpret_cast<u32*>(ws + b);
     b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
     P.items = reinterpret_cast<u32x4*>(ws + b);
-    if (ws_piece_scan >= 1 && ws_piece_scan <= 3) {
-        const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : 16);
+    if (ws_piece_scan >= 1 && ws_piece_scan <= 4) {
+        const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : (ws_piece_scan == 3 ? 16 : 8));
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
-        auto k = G == 64 ? ws_piece_scan_kernel<64> : (G == 32 ? ws_piece_scan_kernel<32> : ws_piece_scan_kernel<16>);
+        auto k = G == 64 ? ws_piece_scan_kernel<64>
+                         : (G == 32 ? ws_piece_scan_kernel<32> : (G == 16 ? ws_piece_scan_kernel<16> : ws_piece_scan_kernel<8>));
         hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                            L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, lo, hi);

@@ -138,6 +138,11 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
 
 typedef u32x4 __attribute__((aligned(1))) u32x4u;
 
+__device__ __forceinline__ u64 rl64(u64 v, u32 i) {          // 64-bit readlane
+    return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, (int)i) |
+           ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), (int)i) << 32);
+}
+
 template <int NT>
 __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned char* __restrict__ buf,
                                                                  unsigned char* __restrict__ out, u32 max_frames,
@@ -227,7 +232,7 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
     const u64* __restrict__ seg_len, WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     unsigned char* __restrict__ out, const u64* __restrict__ out_off, WebsocketMsgDesc_t* __restrict__ msg,
-    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io) {
+    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io, u32 merge) {
     constexpr u32 RSEG_C = (RSEG_L - 1) * 64;         // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[RSEG_L * 64];
     __shared__ BodyL tab[RSEG_TB];
@@ -338,11 +343,27 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
             }
         }
         __syncthreads();
-        // ---- 3. wave wv: the window's part of bodies blo + wv, blo + wv + 4, ...
-        const u32 bhi = sh_bhi;
-        for (u32 bi = sh_blo + wv; bi <= bhi; bi += RSEG_T / 64) {
-            const BodyL b = tab[bi];
-            const u32 key = tkey[bi];
+        // ---- 3. wave wv: the window's part of bodies blo + wv, blo + wv + 4, ... The body table
+        //         goes to registers once (lane i: body i); a body's fields come back by readlane,
+        //         so the loop has no LDS round trips besides the data.
+        const u32 blo = sh_blo, bhi = sh_bhi;
+        const BodyL t = tab[lane];
+        const u32 tk = tkey[lane];
+        // The output chunk holding the boundary between bodies j-1 and j (off the 16-B grid) is
+        // assembled whole by body j's wave when both bodies cover it from this window (one 16-B
+        // store instead of byte stores from two waves): bit j of mg.
+        u64 mg = 0;
+        if (merge) {
+            const u64 px0 = __shfl_up(t.x0, 1, 64), pdst = __shfl_up(t.dst, 1, 64), plen = __shfl_up(t.len, 1, 64);
+            const u64 da = obase + t.dst, C0 = da & ~15ull;
+            const bool ok = lane > blo && lane <= bhi && (da & 15) && t.len && plen >= da - C0 &&
+                            px0 + (C0 - obase - pdst) >= W0 && t.len >= C0 + 16 - da && t.x0 + (C0 + 16 - da) <= W1;
+            mg = __ballot(ok);
+        }
+        for (u32 bi = blo + wv; bi <= bhi; bi += RSEG_T / 64) {
+            BodyL b;
+            b.x0 = rl64(t.x0, bi); b.dst = rl64(t.dst, bi); b.len = rl64(t.len, bi);
+            const u32 key = (u32)__builtin_amdgcn_readlane((int)tk, (int)bi);
             if (!b.len) continue;
             const u64 xa = b.x0 > W0 ? b.x0 : W0, xe = b.x0 + b.len < W1 ? b.x0 + b.len : W1;
             const u64 da = obase + b.dst + (xa - b.x0), de = da + (xe - xa);   // absolute output range
@@ -361,11 +382,36 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
                     st16<1>(w, reinterpret_cast<gu32x4*>(A + ((u64)c << 4)));
                 }
             }
-            // edges: lanes 0-15 the head [da, min(A, de)), lanes 16-31 the tail [max(A, B), de)
+            const bool mh = (mg >> bi) & 1ull, mt = bi < 63 && ((mg >> (bi + 1)) & 1ull);
+            if (mh && lane == 0) {                                           // head chunk: bodies bi-1 and bi
+                const u64 px0 = rl64(t.x0, bi - 1), pdst = rl64(t.dst, bi - 1);
+                const u32 kp = (u32)__builtin_amdgcn_readlane((int)tk, (int)bi - 1);
+                const u64 C0 = da & ~15ull;
+                const u32 sb = (u32)(da - C0);                               // bytes of body bi-1 in it (1..15)
+                // body bi-1's bytes as they sit at chunk positions 0..15, body bi's first 16 bytes
+                const u32 op = (u32)(px0 + (C0 - obase - pdst) - W0), oc = (u32)(b.x0 - W0);
+                u64 p0, p1, c0, c1;
+                ws_hdr_from32(win[op >> 4], win[(op >> 4) + 1], op & 15u, p0, p1);
+                ws_hdr_from32(win[oc >> 4], win[(oc >> 4) + 1], oc & 15u, c0, c1);
+                // shift body bi's bytes up by sb positions (128-bit left shift by 8*sb bits)
+                const u32 sh = 8u * sb;
+                const u64 n0 = sh < 64 ? c0 << sh : 0ull;
+                const u64 n1 = sh < 64 ? (c1 << sh) | (c0 >> (64 - sh)) : c0 << (sh - 64);
+                const u64 m0 = sh < 64 ? (1ull << sh) - 1 : ~0ull;            // byte q < sb: body bi-1
+                const u64 m1 = sh > 64 ? (1ull << (sh - 64)) - 1 : 0ull;
+                const u64 kp64 = (u64)kp | ((u64)kp << 32), kc64 = (u64)key | ((u64)key << 32);
+                const u64 r0 = ((p0 ^ kp64) & m0) | ((n0 ^ kc64) & ~m0);
+                const u64 r1 = ((p1 ^ kp64) & m1) | ((n1 ^ kc64) & ~m1);
+                u32x4 w;
+                w.x = (u32)r0; w.y = (u32)(r0 >> 32); w.z = (u32)r1; w.w = (u32)(r1 >> 32);
+                st16<1>(w, reinterpret_cast<gu32x4*>(C0));
+            }
+            // edges: lanes 0-15 the head [da, min(A, de)), lanes 16-31 the tail [max(A, B), de),
+            // except a boundary chunk assembled whole above (head) or by the next body (tail)
             u64 y = 0;
             bool act = false;
-            if (lane < 16) { y = da + lane; act = y < (A < de ? A : de); }
-            else if (lane < 32) { y = (A > B ? A : B) + (lane - 16); act = y < de; }
+            if (lane < 16) { y = da + lane; act = !mh && y < (A < de ? A : de); }
+            else if (lane < 32) { y = (A > B ? A : B) + (lane - 16); act = !mt && y < de; }
             if (act) {
                 const u32 kb = (key >> (8u * (u32)(y & 3))) & 0xFFu;
                 *reinterpret_cast<gu8*>(y) = (unsigned char)(wb[xa - W0 + (y - da)] ^ kb);
@@ -393,6 +439,8 @@ int ws_reasm_path = 0;
 // fused kernel geometry ("reasm_cfg"): 0 17 KiB windows + 8 waves/SIMD (SGPR spills: slower),
 // 1 17 KiB windows at the compiler's occupancy (7 waves/SIMD, default), 2 19 KiB windows
 int ws_reasm_cfg = 1;
+int ws_reasm_merge = 0;   // "reasm_merge": 1 body-boundary chunks assembled whole by one lane, 0 one
+                          // byte-store instruction from 31 lanes (default: measured faster, cfg5u 1.50 vs 1.65 ms)
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
@@ -413,7 +461,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
         auto k = ws_reasm_cfg == 1 ? ws_reasm_seg_kernel<18, 1>
                                    : (ws_reasm_cfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
         hipLaunchKernelGGL(k, dim3(nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
-                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open);
+                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, (u32)ws_reasm_merge);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);
     }
