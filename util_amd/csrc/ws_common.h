@@ -124,6 +124,25 @@ struct Item {
     u32 rkey, pad;
 };
 
+// Store the bytes of w selected by cov (bit q = byte q) into the 16-B chunk at p: a
+// dword store for every fully selected dword, byte stores only inside partial dwords
+// (one lane issuing 16 byte stores per chunk was measured far slower than 16-B stores).
+__device__ __forceinline__ void ws_store_bytes(WS_GLOBAL unsigned char* p, const u32x4 w, const u32 cov) {
+    WS_GLOBAL u32* const pd = reinterpret_cast<WS_GLOBAL u32*>(p);
+#pragma unroll
+    for (u32 d = 0; d < 4; ++d) {
+        const u32 nib = (cov >> (4 * d)) & 15u;
+        const u32 v = d == 0 ? w.x : (d == 1 ? w.y : (d == 2 ? w.z : w.w));
+        if (nib == 15u) {
+            pd[d] = v;
+        } else if (nib) {
+#pragma unroll
+            for (u32 b = 0; b < 4; ++b)
+                if ((nib >> b) & 1u) p[4 * d + b] = (unsigned char)(v >> (8u * b));
+        }
+    }
+}
+
 __device__ __forceinline__ u32 nib_to_bytemask(u32 n) {
     return ((n & 1u) ? 0x000000FFu : 0u) | ((n & 2u) ? 0x0000FF00u : 0u) | ((n & 4u) ? 0x00FF0000u : 0u) |
            ((n & 8u) ? 0xFF000000u : 0u);
@@ -155,12 +174,7 @@ __device__ __forceinline__ void ws_store_partial(const u32x4 v, gu32x4* const pc
     if (cov == 0xFFFFu) {
         st16<NT>(w, pc);
     } else if (cov) {
-        gu8* const pb = reinterpret_cast<gu8*>(pc);
-#pragma unroll
-        for (u32 q = 0; q < 16; ++q) {
-            const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
-            if ((cov >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
-        }
+        ws_store_bytes(reinterpret_cast<gu8*>(pc), w, cov);
     }
 }
 

@@ -333,12 +333,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
         if (cov[u] == 0xFFFFu || (WHOLE == 1 && ((whole >> u) & 1u)) || (WHOLE == 2 && segcov[u] == 0xFFFFu)) {
             st16<NT>(w, base + c);
         } else {
-            gu8* const pb = reinterpret_cast<gu8*>(base + c);
-#pragma unroll
-            for (u32 q = 0; q < 16; ++q) {
-                const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
-                if ((cov[u] >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
-            }
+            ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
         }
     }
 }

@@ -149,12 +149,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
             if (x >= xseg0 && x + 16 <= xseg1) {
                 st16<NT>(w, pc);                                         // whole chunk inside the segment
             } else {
-                gu8* const pb = reinterpret_cast<gu8*>(pc);
-#pragma unroll
-                for (u32 q = 0; q < 16; ++q) {
-                    const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
-                    if ((cov >> q) & 1u) pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
-                }
+                ws_store_bytes(reinterpret_cast<gu8*>(pc), w, cov);
             }
         }
         const u64 nxt = sh_next;
