@@ -343,6 +343,55 @@ def reasm_fused(wl):
     return wl.fps <= 64 and wl.nseg >= 1024 and wl.wire_bytes <= wl.nseg << 18
 
 
+def run_stream(args, dev, world, rank):
+    """The batch's wire as ONE raw rx stream (a single connection's inbuf, no frame or
+    segment offsets from the host): websocketframeStreamDecodeDevice finds the frame
+    boundaries on the device (speculative grid-wide passes, one 8-byte read per pass) and
+    unmasks with the piece kernel. Same algorithmic bytes as the decode; the call
+    synchronizes its stream (the pass loop reads back the stop word)."""
+    import torch
+    from util_amd import dist as D
+    from util_amd import wsframe as W
+    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank)
+    res = torch.zeros(16, dtype=torch.uint8, device=dev)
+
+    def step():
+        W.stream_decode_device(wl.buf, wl.wire_bytes, wl.nframes, wl.desc, res)
+        wl.decodes += 1
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    wall, step_ms = timed_region(step, args.steps, world)
+    elapsed = D.allreduce([wall], op="max", device=dev)[0]
+    r = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+    bad = int(wl.verify(expect_plain=(wl.decodes % 2 == 1)) != 0)
+    bad += int(int(r["n_frames"]) != wl.nframes or int(r["consumed"]) != wl.wire_bytes or int(r["status"]) != 0)
+    mism = int(D.allreduce([bad], device=dev)[0])
+    mean_kern = step_ms / 1e3
+    out = {
+        "metric": "WebSocket unmask GiB/s of one raw rx stream (device-resident, device-side frame boundaries)",
+        "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
+        "config": {"workload": "one stream: " + Workload.DESCRIPTION[args.config], "config": args.config,
+                   "frames_per_gpu": wl.nframes, "wire_bytes_per_gpu": wl.wire_bytes,
+                   "payload_bytes_per_gpu": wl.payload_bytes},
+        "roofline": {"bound": "hbm", "achieved": round(wl.algo_bytes / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
+                     "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_launch": wl.algo_bytes,
+                     "timed": "HIP events at the two ends of the timed region / steps: ws_stream_pass_kernel "
+                              "passes (host reads the stop word after each) + ws_piece_unmask_kernel",
+                     "kernel_ms_mean": round(step_ms, 4)},
+        "verified": mism == 0,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    return mism
+
+
 def run_reasm(args, dev, world, rank):
     """Fused decode + message reassembly: the wire stays in HBM
     untouched, every message body is gathered unmasked into a contiguous output region.
@@ -523,9 +572,10 @@ def main():
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
-    ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm"],
-                    help="decode (the headline), client-side encode + mask of the same frames, or fused "
-                         "decode + message reassembly (use with --config cfg5)")
+    ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm", "stream"],
+                    help="decode (the headline), client-side encode + mask of the same frames, fused "
+                         "decode + message reassembly (use with --config cfg5), or the whole batch as ONE raw "
+                         "rx stream with no frame offsets (device-side boundary discovery)")
     args = ap.parse_args()
     from util_amd import wsframe as W
     path = DEFAULT_PATH if args.path is None else args.path
@@ -542,8 +592,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    if args.op in ("encode", "reasm"):
-        mism = (run_encode if args.op == "encode" else run_reasm)(args, dev, world, rank)
+    if args.op in ("encode", "reasm", "stream"):
+        mism = {"encode": run_encode, "reasm": run_reasm, "stream": run_stream}[args.op](args, dev, world, rank)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)
