@@ -116,7 +116,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
 // its items, descriptors and piece pointers are written by the lanes in parallel.
 // Small G keeps more segments in flight per wave (the walk is latency-bound).
 #define PSCAN_T 256
-template <int G>
+template <int G, int DBG = 0>
 __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned char* __restrict__ buf,
                                                                 const u64* __restrict__ seg_off,
                                                                 const u64* __restrict__ seg_len, u32 nseg,
@@ -181,10 +181,12 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
         if (gl < ntake) {                                                   // consumed frames, in parallel
-            put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0,
-                     rotl32(h.key, 8u * (u32)(p0 & 3)));
-            put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
-            if (h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
+            if (!(DBG & 4)) {
+                put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0,
+                         rotl32(h.key, 8u * (u32)(p0 & 3)));
+                put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
+            }
+            if (!(DBG & 2) && h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
         }
         const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
         if (ntake) walked_end = fe_last;
@@ -355,6 +357,7 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 
 // Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *disorder_out = the word a gated
 // fallback walker compares with `gen`.
+extern int ws_dbg_flags;
 int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
 
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
@@ -377,6 +380,10 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
         auto k = G == 64 ? ws_piece_scan_kernel<64>
                          : (G == 32 ? ws_piece_scan_kernel<32> : (G == 16 ? ws_piece_scan_kernel<16> : ws_piece_scan_kernel<8>));
+        // A/B tooling only (results wrong): "debug" bit 1 skips descriptor stores, bit 2 items + pointers
+        if (G == 16 && (ws_dbg_flags & 6))
+            k = (ws_dbg_flags & 6) == 2 ? ws_piece_scan_kernel<16, 2>
+                                        : ((ws_dbg_flags & 6) == 4 ? ws_piece_scan_kernel<16, 4> : ws_piece_scan_kernel<16, 6>);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                            L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, lo, hi);
