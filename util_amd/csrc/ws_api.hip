@@ -22,6 +22,7 @@ extern int ws_reasm_path;
 extern int ws_reasm_cfg;
 extern int ws_segfuse_cfg;
 extern int ws_encode_side;
+extern int ws_encode_fused;
 extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_reasm_merge;
@@ -69,6 +70,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "reasm_cfg")) ws_reasm_cfg = (int)value;
     else if (!strcmp(name, "segfuse_cfg")) ws_segfuse_cfg = (int)value;
     else if (!strcmp(name, "encode_side")) ws_encode_side = (int)value;
+    else if (!strcmp(name, "encode_fused")) ws_encode_fused = (int)value;
     else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;

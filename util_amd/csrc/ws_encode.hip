@@ -91,7 +91,80 @@ __device__ __forceinline__ void put_byte(u32x4& w, u32 b, u32 v) {
 
 typedef u32x4 __attribute__((aligned(1))) u32x4u;
 
-template <int NT>
+// Fast edge path of frame i (payload >= 32 B, its extent not clipped, and a next payload
+// entering its tail chunk >= 16 B long): the head chunk [X0, +16) = header + payload
+// bytes [0, 16) (only if the header reaches past X0), the tail chunk [XT, +16) = payload
+// bytes [len-16, len) + the next frame's header (+ its payload bytes [0, 16)). Frame-
+// local, so E3 (which stores these chunks for eligible frames) and E4 (which skips them)
+// agree on it. nx: frame i+1's record (unused when i+1 == n).
+__device__ __forceinline__ bool enc_edge_eligible(const EncFrame& e, const EncFrame& nx, u32 i, u32 n, u64 lead0,
+                                                  u64 out_lo, u64 out_hi) {
+    const u64 o = e.off + lead0, d1 = o + e.hl + e.len, XT = d1 & ~15ull;
+    if (!(e.len >= 32 && (i > 0 || (o & 15) == 0) && o >= out_lo && XT + 16 <= out_hi)) return false;
+    const bool npay = (d1 & 15) && i + 1 < n && d1 + nx.hl < XT + 16;
+    return !npay || nx.len >= 16;
+}
+
+// Assemble and store the eligible frame's head / tail chunks that start in [rlo, rhi)
+// (origin-relative): the 16-B source windows they need are loaded together.
+__device__ __forceinline__ void enc_edge_store(const unsigned char* __restrict__ src, gu32x4* base,
+                                               const EncFrame& e, const EncFrame& nx, bool nxt, u64 lead0,
+                                               u64 rlo, u64 rhi) {
+    const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
+    const u64 X0 = (o + 15) & ~15ull, XT = d1 & ~15ull;
+    const bool head = X0 < d0 && X0 >= rlo && X0 < rhi, tail = (d1 & 15) != 0 && XT >= rlo && XT < rhi;
+    const u64 dn0 = d1 + nx.hl;                                          // next payload start
+    const bool npay = tail && nxt && dn0 < XT + 16;                      // next payload enters the tail chunk
+    u32x4 wh = {0, 0, 0, 0}, wt = {0, 0, 0, 0}, wn = {0, 0, 0, 0};
+    if (head) wh = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src));
+    if (tail) wt = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src + e.len - 16));
+    if (npay) wn = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + nx.src));
+    const u32 kh = e.masked ? e.key : 0u, kn = nx.masked ? nx.key : 0u;
+    if (head) {                                                          // head chunk holds header bytes
+        u32x4 w = {0, 0, 0, 0};
+        for (u32 q = 0; q < 16; ++q) {
+            const u64 y = X0 + q;
+            u32 v;
+            if (y < d0) {
+                v = enc_header_byte(e, (u32)(y - o));
+            } else {
+                const u32 pi = (u32)(y - d0);
+                const u32 wq = pi < 4 ? wh.x : (pi < 8 ? wh.y : (pi < 12 ? wh.z : wh.w));
+                v = ((wq >> (8u * (pi & 3))) ^ (kh >> (8u * (pi & 3)))) & 0xFFu;
+            }
+            put_byte(w, q, v);
+        }
+        base[X0 >> 4] = w;
+    }
+    if (tail) {                                                          // tail chunk: this + next frame
+        u32x4 w = {0, 0, 0, 0};
+        u32 cov = 0;
+        for (u32 q = 0; q < 16; ++q) {
+            const u64 y = XT + q;
+            u32 v;
+            if (y < d1) {
+                const u64 pi = y - d0;
+                const u32 t = (u32)(pi - (e.len - 16));
+                const u32 wq = t < 4 ? wt.x : (t < 8 ? wt.y : (t < 12 ? wt.z : wt.w));
+                v = ((wq >> (8u * (t & 3))) ^ (kh >> (8u * (u32)(pi & 3)))) & 0xFFu;
+            } else if (!nxt) {
+                continue;                                                // past the batch
+            } else if (y < dn0) {
+                v = enc_header_byte(nx, (u32)(y - d1));
+            } else {
+                const u32 pi = (u32)(y - dn0);
+                const u32 wq = pi < 4 ? wn.x : (pi < 8 ? wn.y : (pi < 12 ? wn.z : wn.w));
+                v = ((wq >> (8u * (pi & 3))) ^ (kn >> (8u * (pi & 3)))) & 0xFFu;
+            }
+            put_byte(w, q, v);
+            cov |= 1u << q;
+        }
+        if (cov == 0xFFFFu) base[XT >> 4] = w;
+        else ws_store_bytes(reinterpret_cast<gu8*>(base + (XT >> 4)), w, cov);
+    }
+}
+
+template <int NT, int FUSED>
 __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char* __restrict__ src,
                                                             const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
                                                             const u64* __restrict__ wire_off,
@@ -102,6 +175,7 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
     const u64 total = min(wire_off[n], capacity);                            // never write past the capacity
+    const u64 out_lo = lead0, out_hi = lead0 + total;                        // origin-relative output
     const u64 r0 = (((u64)blockIdx.x << ENC_SHIFT) + (u64)wv * (64 * ENC_U * 16));  // origin-relative
     const u64 r1 = r0 + 64 * ENC_U * 16;
     const u32 first = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
@@ -147,8 +221,23 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
                     fkey[u] = rk;
                     continue;
                 }
-                // chunks with header bytes or a frame edge: ws_enc_edge_kernel
+                // chunks with header bytes or a frame edge: below (FUSED) or ws_enc_edge_kernel
             }
+        }
+        if (FUSED) {
+            // edge chunks of this batch's eligible frames that start in this wave's range: the
+            // next frame's record from lane + 1 (the batch's last lane loads it); the source
+            // windows are mostly lines this block is streaming anyway
+            EncFrame nx;
+            nx.src = __shfl_down(e.src, 1, 64); nx.len = __shfl_down(e.len, 1, 64);
+            nx.off = __shfl_down(e.off, 1, 64); nx.key = __shfl_down(e.key, 1, 64);
+            nx.hl = __shfl_down(e.hl, 1, 64); nx.b0 = __shfl_down(e.b0, 1, 64);
+            nx.masked = __shfl_down(e.masked, 1, 64);
+            const bool nxt = j + 1 < n;
+            const bool mine = valid && lane < nlim && ee > r0;
+            if (mine && lane == 63 && nxt) nx = enc_load(f, wire_off, j + 1);
+            if (mine && enc_edge_eligible(e, nx, j, n, lead0, out_lo, out_hi))
+                enc_edge_store(src, base, e, nx, nxt, lead0, r0, r1);
         }
         if (nlim < 64) break;
         k += 64;
@@ -160,7 +249,6 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
         v[u] = (u32x4){0, 0, 0, 0};
         if (kind[u] == 1) v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + fsrc[u]));
     }
-    const u64 out_hi = lead0 + total;                                        // origin-relative end
 #pragma unroll
     for (int u = 0; u < ENC_U; ++u) {
         const u64 x = r0 + (u64)(u * 1024 + lane * 16);
@@ -175,7 +263,8 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
 __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* __restrict__ src,
                                                           const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
                                                           const u64* __restrict__ wire_off,
-                                                          unsigned char* __restrict__ dst, u64 capacity) {
+                                                          unsigned char* __restrict__ dst, u64 capacity,
+                                                          u32 enc_fused) {
     const u32 i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
@@ -184,81 +273,14 @@ __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* _
     const u64 out_lo = lead0, out_hi = lead0 + total;
     const EncFrame e = enc_load(f, wire_off, i);
     const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
-    // Fast path (payload >= 32 B, nothing clipped): the head chunk [X0, +16) = header +
-    // payload bytes [0, 16) (only if the header reaches past X0), the tail chunk [XT, +16)
-    // = payload bytes [len-16, len) + the next frame's header (+ its payload bytes [0, 16),
-    // which must then be >= 16 B long): the next record and the 16-B source windows a
-    // chunk needs are loaded together, one round trip after this frame's record.
-    {
-        const u64 X0 = (o + 15) & ~15ull, XT = d1 & ~15ull;
-        const bool nxt = i + 1 < n, head = X0 < d0, tail = (d1 & 15) != 0;
-        if (e.len >= 32 && (i > 0 || (o & 15) == 0) && o >= out_lo && XT + 16 <= out_hi) {
-            EncFrame nx = {};
-            u32x4 wh = {0, 0, 0, 0}, wt = {0, 0, 0, 0}, wn = {0, 0, 0, 0};
-            if (tail && nxt) nx = enc_load(f, wire_off, i + 1);
-            if (head) wh = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src));
-            if (tail)
-                wt = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src + e.len - 16));
-            const u64 dn0 = d1 + nx.hl;                                      // next payload start
-            const bool npay = tail && nxt && dn0 < XT + 16;                  // next payload enters the tail chunk
-            if (npay && nx.len < 16) goto generic;
-            if (npay) wn = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + nx.src));
-            const u32 kh = e.masked ? e.key : 0u, kn = nx.masked ? nx.key : 0u;
-            if (head) {                                                      // head chunk holds header bytes
-                u32x4 w = {0, 0, 0, 0};
-                for (u32 q = 0; q < 16; ++q) {
-                    const u64 y = X0 + q;
-                    u32 v;
-                    if (y < d0) {
-                        v = enc_header_byte(e, (u32)(y - o));
-                    } else {
-                        const u32 pi = (u32)(y - d0);
-                        const u32 wq = pi < 4 ? wh.x : (pi < 8 ? wh.y : (pi < 12 ? wh.z : wh.w));
-                        v = ((wq >> (8u * (pi & 3))) ^ (kh >> (8u * (pi & 3)))) & 0xFFu;
-                    }
-                    put_byte(w, q, v);
-                }
-                base[X0 >> 4] = w;
-            }
-            if (tail) {                                                      // tail chunk: this + next frame
-                u32x4 w = {0, 0, 0, 0};
-                u32 cov = 0;
-                for (u32 q = 0; q < 16; ++q) {
-                    const u64 y = XT + q;
-                    u32 v;
-                    if (y < d1) {
-                        const u64 pi = y - d0;
-                        const u32 t = (u32)(pi - (e.len - 16));
-                        const u32 wq = t < 4 ? wt.x : (t < 8 ? wt.y : (t < 12 ? wt.z : wt.w));
-                        v = ((wq >> (8u * (t & 3))) ^ (kh >> (8u * (u32)(pi & 3)))) & 0xFFu;
-                    } else if (!nxt) {
-                        continue;                                            // past the batch
-                    } else if (y < dn0) {
-                        v = enc_header_byte(nx, (u32)(y - d1));
-                    } else {
-                        const u32 pi = (u32)(y - dn0);
-                        const u32 wq = pi < 4 ? wn.x : (pi < 8 ? wn.y : (pi < 12 ? wn.z : wn.w));
-                        v = ((wq >> (8u * (pi & 3))) ^ (kn >> (8u * (pi & 3)))) & 0xFFu;
-                    }
-                    put_byte(w, q, v);
-                    cov |= 1u << q;
-                }
-                gu32x4* const pc = base + (XT >> 4);
-                if (cov == 0xFFFFu) {
-                    *pc = w;
-                } else {
-                    gu8* const pb = reinterpret_cast<gu8*>(pc);
-                    for (u32 q = 0; q < 16; ++q) {
-                        if (!((cov >> q) & 1u)) continue;
-                        const u32 wq = q < 4 ? w.x : (q < 8 ? w.y : (q < 12 ? w.z : w.w));
-                        pb[q] = (unsigned char)(wq >> (8u * (q & 3)));
-                    }
-                }
-            }
-            return;
-        }
+    // eligible frames: E3 stored their edge chunks (enc_edge_eligible / enc_edge_store)
+    EncFrame nx = {};
+    if (i + 1 < n) nx = enc_load(f, wire_off, i + 1);
+    if (enc_fused && enc_edge_eligible(e, nx, i, n, lead0, out_lo, out_hi)) return;
+    if (!enc_fused && enc_edge_eligible(e, nx, i, n, lead0, out_lo, out_hi)) {
+        enc_edge_store(src, base, e, nx, i + 1 < n, lead0, 0, ~0ull);
+        return;
     }
-generic:
     u64 X = i ? ((o + 15) & ~15ull) : (o & ~15ull);                           // first chunk start owned
     const u64 lim = d1 < out_hi ? d1 : out_hi;                               // interior chunks end here
     for (; X < d1 && X < out_hi; X += 16) {
@@ -338,6 +360,8 @@ static int enc_side(EncSide** out) {
     *out = &S;
     return 0;
 }
+int ws_encode_fused = 0;  // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
+                          // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
 int ws_encode_side = 0;   // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
                           // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
@@ -371,7 +395,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         if ((e = hipEventRecord(S->fork, st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
         if ((e = hipStreamWaitEvent(S->s, S->fork, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
         hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, S->s, d_src, d_frames,
-                           nframes, d_wire_off, d_dst, (u64)dst_capacity);
+                           nframes, d_wire_off, d_dst, (u64)dst_capacity, 0u);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
         if ((e = hipEventRecord(S->join, S->s)) != hipSuccess) return ws_set_err("hipEventRecord", e);
     }
@@ -379,8 +403,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
                        d_wire_off, ptr, lead0, npieces);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     if (npieces) {
-        hipLaunchKernelGGL((ws_enc_copy_kernel<1>), dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
-                           d_wire_off, ptr, d_dst, (u64)dst_capacity);
+        auto copy = ws_encode_fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
+        hipLaunchKernelGGL(copy, dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes, d_wire_off, ptr,
+                           d_dst, (u64)dst_capacity);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
     if (S) {
@@ -388,7 +413,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         return 0;
     }
     hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, d_src, d_frames, nframes,
-                       d_wire_off, d_dst, (u64)dst_capacity);
+                       d_wire_off, d_dst, (u64)dst_capacity, (u32)(ws_encode_fused && npieces));
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
     return 0;
 }
