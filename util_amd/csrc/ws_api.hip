@@ -218,6 +218,16 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     if (path == 3) {
         const u32 gen = ws_next_gen();
         const u32* disorder = nullptr;
+        // A/B tooling only: "debug" bit 3 reruns K2 on the previous call's scan (same batch)
+        static bool s_scanned = false;
+        if ((ws_dbg_flags & 8) && s_scanned) {
+            PieceWs P;
+            extern int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, PieceWs* out);
+            if ((rc = ws_piece_rescan_views(L, lo, hi, reinterpret_cast<unsigned char*>(ws), &P))) return rc;
+            extern int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
+            return ws_launch_piece_unmask(L, P, t.nt, gen);
+        }
+        s_scanned = true;
         if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder))) return rc;
         // fallback for segments out of buffer order: a small gated walker grid (exits at once otherwise)
         return ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen);

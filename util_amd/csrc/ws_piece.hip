@@ -398,6 +398,25 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     return 0;
 }
 
+// the workspace views of an already scanned batch (A/B tooling: K2 without K1)
+int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, PieceWs* out) {
+    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
+    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
+    PieceWs P;
+    P.npieces = piece_count(lo_org, hi_org);
+    P.pbase = lo_org >> PIECE_SHIFT;
+    P.c_lo = lo_org >> 4;
+    P.c_hi = (hi_org + 15) >> 4;
+    P.disorder = reinterpret_cast<u32*>(ws);
+    P.ptr = reinterpret_cast<u64*>(ws + 16);
+    size_t b = (16 + P.npieces * 8 + 15) & ~(size_t)15;
+    P.nwork = reinterpret_cast<u32*>(ws + b);
+    b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
+    P.items = reinterpret_cast<u32x4*>(ws + b);
+    *out = P;
+    return 0;
+}
+
 // K2 alone over the pieces of a scanned batch
 int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
