@@ -27,8 +27,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICRO
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
 KERNELS = {0: "ws_segblock_kernel", 1: "ws_walker_kernel", 2: "ws_unmask_kernel", 3: "ws_piece_unmask_kernel",
            4: "ws_segfuse_kernel"}
-STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel + gated ws_walker_kernel (exits at once "
-                   "for ordered segments)",
+STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel (which decodes unordered batches itself, "
+                   "one wave per segment)",
                 4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)"}
 DEFAULT_PATH = -1  # auto: 4 (segfuse) for >= 1024 segments of <= 17 KiB - 64 B average, max_frames <= 64; else 3
 

@@ -228,9 +228,12 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
             return ws_launch_piece_unmask(L, P, t.nt, gen);
         }
         s_scanned = true;
-        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder))) return rc;
-        // fallback for segments out of buffer order: a small gated walker grid (exits at once otherwise)
-        return ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen);
+        bool fallback = false;
+        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder, &fallback)))
+            return rc;
+        // segments out of buffer order are decoded by K2's fallback; with no pieces to launch K2
+        // on, a small gated walker grid does it (exits at once for ordered batches)
+        return fallback ? ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen) : 0;
     }
     const size_t nslots = (size_t)nseg * max_frames;
     u32* keys = reinterpret_cast<u32*>(ws);

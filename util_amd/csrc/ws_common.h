@@ -317,7 +317,8 @@ struct PieceWs {          // ws_piece.hip workspace views after K1
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out);
 u32 ws_next_gen();
 int ws_device_workspace(size_t bytes, hipStream_t stream, void** out);
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out);
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
+                    bool* fallback_needed);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
 // (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes whose
 // first 16 bytes were zeroed once after allocation, else the per-device one is used

@@ -23,7 +23,7 @@
 //   touched by exactly one block, so no byte is stored twice.
 // Fallback: if the segments are not in ascending buffer order, K2 stores nothing and a
 //   gated walker (ws_walker.hip) decodes the batch.
-#include "ws_common.h"
+#include "ws_walk.h"
 
 #define PIECE_T 256
 #define PIECE_U 4
@@ -229,7 +229,9 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   const u32* __restrict__ nwork,
                                                                   const u64* __restrict__ ptr,
                                                                   const u32* __restrict__ disorder, u32 gen, u64 pbase,
-                                                                  u64 c_lo, u64 c_hi) {
+                                                                  u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
+                                                                  WebsocketFrameDesc_t* __restrict__ desc,
+                                                                  WebsocketSegResult_t* __restrict__ res) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 pc0 = (pbase + blockIdx.x) << (PIECE_SHIFT - 4);              // first chunk of the piece
@@ -338,6 +340,12 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
             ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
         }
     }
+    // K1 found the segments out of buffer order (or outside [lo, hi)): nothing was stored
+    // above; the batch is decoded here instead, one wavefront per segment (ws_walk.h)
+    if (!ok) {
+        for (u32 s2 = blockIdx.x * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
+            walk_segment<4, NT>(buf, s2, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
+    }
 }
 
 // ws layout: [disorder u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
@@ -433,17 +441,21 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
     if (ws_piece_occ == 7 || ws_piece_occ == 8)           // forced occupancy: spills, measured slower
         k = ws_piece_occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
     hipLaunchKernelGGL(k, dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                       L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi);
+                       L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
+                       L.desc, L.res);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
 }
 
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out) {
+// K1 + K2; K2 also holds the fallback for unordered batches. *fallback_needed: no K2
+// was launched (no pieces), so the caller must launch the gated walker itself.
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
+                    bool* fallback_needed) {
     PieceWs P;
     int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P);
     if (rc) return rc;
     if ((rc = ws_launch_piece_unmask(L, P, nt, gen))) return rc;
-    u32* disorder = P.disorder;
-    *disorder_out = disorder;
+    *disorder_out = P.disorder;
+    *fallback_needed = P.npieces == 0;
     return 0;
 }
