@@ -587,11 +587,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; WS_BENCH_RANKS_PER_GPU > 1 rehearses the multi-rank path on fewer GPUs
+    # (ranks share a device; RCCL needs distinct devices, so that rehearsal runs over gloo)
+    per_gpu = int(os.environ.get("WS_BENCH_RANKS_PER_GPU", "1"))
+    gpu = local // per_gpu
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if per_gpu > 1:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu)
     if args.op in ("encode", "reasm", "stream"):
         mism = {"encode": run_encode, "reasm": run_reasm, "stream": run_stream}[args.op](args, dev, world, rank)
         if world > 1:

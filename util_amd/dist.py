@@ -39,6 +39,8 @@ def allreduce(values, op="sum", device=None):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return list(values)
+    if dist.get_backend() == "gloo":
+        device = None                                  # gloo reduces host tensors
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return t.tolist()
