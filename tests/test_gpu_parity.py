@@ -293,3 +293,31 @@ def test_device_unordered_and_out_of_range(dev):
     od, orr = oracle_segments(ob, so, sl, 8)
     assert np.array_equal(res.cpu().numpy().view(W.SEGRES_DTYPE), orr)
     assert np.array_equal(d[:n].cpu().numpy(), ob)
+
+
+@pytest.mark.parametrize("total", [(1 << 31) + 6, 1 << 32])
+def test_int_truncation_real_size(dev, decode_path, total):
+    """frames whose length sum reaches 2^31 (the (int) return goes negative: unmasked, then
+    an error, websocketframe.c:164 + net_reactor.c:518-520) and exactly 2^32 (the return
+    truncates to 0: unmasked, not consumed), at their real sizes, vs the oracle"""
+    if decode_path == -1:
+        pytest.skip("auto == piece for one segment")
+    plen = total - 14
+    n = total + 100
+    block = np.random.default_rng(7).integers(0, 256, (1 << 20) + 7, dtype=np.uint8)
+    host = np.empty(n, dtype=np.uint8)
+    for a in range(0, n, len(block)):                     # tiled random bytes: cheap at 4 GB
+        host[a:a + len(block)] = block[:n - a]
+    host[:14] = np.frombuffer(bytes([0x82, 0x80 | 127]) + plen.to_bytes(8, "big") + bytes([0x11, 0x22, 0x33, 0x44]),
+                              dtype=np.uint8)
+    gb, gd, gr = gpu_decode(dev, host.copy(), [0], [n], 4)
+    ob = host.copy()
+    od, orr = oracle_segments(ob, [0], [n], 4)
+    assert np.array_equal(gr, orr)
+    assert np.array_equal(used_descs(gd, gr, 4), used_descs(od, orr, 4))
+    assert np.array_equal(gb, ob)
+    if total < (1 << 32):
+        assert int(gr[0]["status"]) == -1 and int(gr[0]["n_frames"]) == 1 and int(gd[0]["ret"]) < 0
+    else:
+        assert int(gr[0]["n_frames"]) == 0 and int(gr[0]["consumed"]) == 0
+    del gb, ob, host

@@ -194,3 +194,18 @@ def test_reassemble_length_quirks(dev):
     _, orr, _, _, _ = oracle_reassemble(wire, so, sl, 16)
     assert (orr["status"] == -3).any() and (orr["status"] == -2).any()
     check(dev, wire, so, sl, 16, tag="quirks")
+
+
+@pytest.mark.parametrize("total", [(1 << 31) + 6, 1 << 32])
+def test_reassemble_int_truncation_real_size(dev, total):
+    """a frame whose length sum reaches 2^31 (negative (int) return: descriptor, decode error,
+    no body) or exactly 2^32 (return 0: not consumed) at its real size, vs the oracle"""
+    plen = total - 14
+    n = total + 100
+    block = np.random.default_rng(8).integers(0, 256, (1 << 20) + 7, dtype=np.uint8)
+    wire = np.empty(n, dtype=np.uint8)
+    for a in range(0, n, len(block)):
+        wire[a:a + len(block)] = block[:n - a]
+    wire[:14] = np.frombuffer(bytes([0x02, 0x80 | 127]) + plen.to_bytes(8, "big") + bytes([1, 2, 3, 4]), dtype=np.uint8)
+    _, oms, _ = check(dev, wire, [0], [n], 4, out_size=1 << 20, tag="int truncation")
+    assert oms == [[]]
