@@ -127,3 +127,17 @@ def test_host_decode_word_xor_matches_bytewise():
             r, doff, dl, fin, typ = W.websocketframeDecode(buf, len(frame), align)
             assert r == len(frame) and dl == plen
             assert bytes(buf[align + hl + 4:]) == pay.tobytes()
+
+
+def test_c_program_links_and_runs(tmp_path):
+    """a C caller of the reference API (tests/c/drop_in.c), compiled against
+    include/wsframe_amd.h and linked to libwsframe_amd.so in place of websocketframe.c"""
+    util_amd.load_lib()
+    exe = str(tmp_path / "drop_in")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "c", "drop_in.c"), "-L", libdir, "-lwsframe_amd",
+                    "-Wl,-rpath," + libdir, "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "drop_in ok"
