@@ -110,9 +110,11 @@ class Workload:
     }
 
     @classmethod
-    def make(cls, name, dev, nframes=None, seed_offset=0):
+    def make(cls, name, dev, nframes=None, seed_offset=0, fps=None, plen=None):
         from util_amd import synth
-        n, pk, fl, bk, seed, fps = cls.CONFIGS[name]
+        n, pk, fl, bk, seed, fps0 = cls.CONFIGS[name]
+        fps = fps or fps0
+        fl = plen or fl
         if nframes is not None:
             n = nframes
         return cls(name, dev, n, pk, fl, bk, seed + seed_offset, fps, synth)
@@ -572,6 +574,8 @@ def main():
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
+    ap.add_argument("--fps", type=int, default=None, help="override frames per rx segment (experiments)")
+    ap.add_argument("--plen", type=int, default=None, help="override the fixed payload length (experiments)")
     ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm", "stream"],
                     help="decode (the headline), client-side encode + mask of the same frames, fused "
                          "decode + message reassembly (use with --config cfg5), or the whole batch as ONE raw "
@@ -605,7 +609,8 @@ def main():
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)
 
-    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank)
+    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank, fps=args.fps,
+                       plen=args.plen)
     torch.cuda.synchronize()
     sample = None
     if rank == 0 and world == 1 and not args.no_cpu:
