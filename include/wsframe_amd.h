@@ -158,7 +158,8 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
  * after d_buf + len. Frame boundaries are found by grid-wide speculative passes (one
  * pass per change of frame length, each ends with an 8-byte device-to-host read), so
  * the call synchronizes hip_stream; streams whose lengths keep changing finish in a
- * single-wavefront walk. Returns 0 or a negative error. */
+ * chunk-parallel walk (>= 16 MiB left: speculative entries per 4 MiB chunk, each chunk
+ * written by one wavefront) or a single-wavefront walk. Returns 0 or a negative error. */
 WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,
                                                         unsigned int max_frames, WebsocketFrameDesc_t* d_desc,
                                                         WebsocketSegResult_t* d_res, void* hip_stream);
@@ -175,6 +176,12 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * "blocks_per_cu" (0 = resident limit). Returns 0, or -1 for an unknown name. Not
  * thread-safe against concurrent calls. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
+
+/* Counters of the calling process's most recent call (diagnostics): "stream_rw_chunks"
+ * (chunks of a long stream written from the chunk-parallel walk's records),
+ * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront). Returns 0, or -1
+ * for an unknown name. */
+WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value);
 
 /* ---- Part 2b: fused decode + fragmented-message reassembly -- */
 

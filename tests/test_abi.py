@@ -24,7 +24,7 @@ def header_symbols():
 def test_exports_every_declared_symbol():
     util_amd.load_lib()
     declared = header_symbols()
-    assert len(declared) == 18
+    assert len(declared) == 19
     assert sorted(_lib.EXPORTS) == declared
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\bT (websocketframe\w+)", out))

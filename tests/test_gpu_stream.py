@@ -72,3 +72,116 @@ def test_stream_max_frames(dev):
     wire, *_ = wsynth.make_batch(5000, 0, 1000, 0, 4)
     r = run(dev, wire, 1234)
     assert int(r["n_frames"]) == 1234 and int(r["status"]) == W.SEG_MAX_FRAMES
+
+
+# --- long streams whose lengths change every frame: the chunk-parallel walk ------------------
+# (ws_stream.hip R1-R3; streams of >= 16 MiB after the grid passes stop paying)
+
+def long_stream(rng, nbytes, pick, masked=0.999, b0=None, payload=None):
+    """frames back to back until about nbytes: pick(rng) -> payload length; b0 None = a
+    client opcode (text/binary/continuation, FIN random); payload(rng, n) -> bytes"""
+    parts, total = [], 0
+    while total < nbytes:
+        plen = int(pick(rng))
+        key = rng.integers(0, 256, 4, dtype=np.uint8) if rng.random() < masked else None
+        first = b0 if b0 is not None else int(rng.choice([0x00, 0x01, 0x02, 0x80, 0x81, 0x82, 0x89, 0x8A]))
+        m = 0x80 if key is not None else 0
+        if plen < 126:
+            h = bytes([first, m | plen])
+        elif plen <= 0xFFFF:
+            h = bytes([first, m | 126]) + plen.to_bytes(2, "big")
+        else:
+            h = bytes([first, m | 127]) + plen.to_bytes(8, "big")
+        if key is not None:
+            h += key.tobytes()
+        body = payload(rng, plen) if payload else rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        parts.append(h + body)
+        total += len(h) + plen
+    return np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+
+
+def mix3(rng):
+    return rng.choice([125, 1500, 65536])
+
+
+@pytest.fixture
+def serial_walk():
+    """the same stream through the one-wavefront walk, for a before/after check"""
+    W.set_option("stream_rw", 0)
+    yield
+    W.set_option("stream_rw", 1)
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_long_stream_cfg3_mix(dev, shift):
+    """the cfg3 length mix as one 48 MiB client stream (4 MiB chunks)"""
+    wire = long_stream(np.random.default_rng(21), 48 << 20, mix3, masked=1.0)
+    r = run(dev, wire, 1 << 16, shift)
+    assert int(r["consumed"]) == len(wire) and int(r["status"]) == W.SEG_OK
+    # every chunk from the speculative records (no one-wavefront chunk walks; an unmasked
+    # frame in a client stream would end its chunk's speculation)
+    assert W.get_stat("stream_rw_chunks") >= 11 and W.get_stat("stream_rw_chunk_walks") == 0
+
+
+def test_long_stream_small_frames(dev):
+    """0..300 B frames: chunks shrink to keep about a thousand frames each"""
+    wire = long_stream(np.random.default_rng(22), 20 << 20, lambda g: g.integers(0, 301))
+    r = run(dev, wire, 1 << 18)
+    assert int(r["consumed"]) == len(wire)
+
+
+def test_long_stream_frames_longer_than_window(dev):
+    """frames of 100 KiB - 1 MiB: chunk entries outside the candidate window, chunk walks"""
+    wire = long_stream(np.random.default_rng(23), 40 << 20, lambda g: g.integers(100 << 10, 1 << 20))
+    r = run(dev, wire, 1 << 12)
+    assert int(r["consumed"]) == len(wire)
+
+
+def test_long_stream_unmasked_and_mixed(dev):
+    """server frames (no MASK) and a stream that mixes both"""
+    run(dev, long_stream(np.random.default_rng(24), 24 << 20, mix3, masked=0.0), 1 << 14)
+    run(dev, long_stream(np.random.default_rng(25), 24 << 20, mix3, masked=0.7), 1 << 14)
+
+
+def test_long_stream_nested_frames(dev):
+    """payloads made of valid client frames: speculative walks that look like the chain
+    (slot overflow, merged walks) must not change the result"""
+    def inner(rng, n):
+        out = bytearray()
+        while len(out) < n:
+            k = int(rng.integers(0, 120))
+            out += bytes([0x82, 0x80 | k]) + rng.integers(0, 256, 4 + k, dtype=np.uint8).tobytes()
+        return bytes(out[:n])
+    wire = long_stream(np.random.default_rng(26), 24 << 20, lambda g: g.integers(2000, 40000), payload=inner)
+    r = run(dev, wire, 1 << 14)
+    assert int(r["consumed"]) == len(wire)
+
+
+@pytest.mark.parametrize("cut", ["max_frames", "truncated", "garbage", "error"])
+def test_long_stream_endings(dev, cut):
+    """the walk ending inside the parallel part: MAX_FRAMES, an incomplete last frame,
+    random bytes inserted mid-stream, a LEN_WRAP / decode-error header mid-stream"""
+    rng = np.random.default_rng(27)
+    wire = long_stream(rng, 32 << 20, mix3)
+    max_frames = 1 << 16
+    if cut == "max_frames":
+        max_frames = 1200
+    elif cut == "truncated":
+        wire = wire[:len(wire) - 1000].copy()
+    elif cut == "garbage":
+        at = 20 << 20
+        wire = np.concatenate([wire[:at], rng.integers(0, 256, 37, dtype=np.uint8), wire[at:]])
+    else:
+        # a 64-bit length with the top bit set at the first frame start after 25 MiB
+        od, orr = oracle_segments(wire.copy(), [0], [len(wire)], 1 << 16)
+        fo = od["frame_off"][:int(orr[0]["n_frames"])]
+        at = int(fo[np.searchsorted(fo, 25 << 20)])
+        bad = bytes([0x82, 0xFF]) + (0xFFFFFFFFFFFFFFF0).to_bytes(8, "big") + bytes(4)
+        wire = np.concatenate([wire[:at], np.frombuffer(bad, dtype=np.uint8), wire[at:]])
+    run(dev, wire, max_frames)
+
+
+def test_long_stream_same_as_serial(dev, serial_walk):
+    """the one-wavefront walk on a chunk-parallel-sized stream (the option's other side)"""
+    wire = long_stream(np.random.default_rng(28), 17 << 20, mix3)
+    run(dev, wire, 1 << 14)

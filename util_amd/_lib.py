@@ -29,7 +29,8 @@ EXPORTS = [
     "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
     "websocketframeEncode", "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
     "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice", "websocketframeStreamDecodeDevice",
-    "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuCalibrate", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
+    "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuGetStat",
+    "websocketframeGpuCalibrate", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
 ]
 
 
@@ -80,6 +81,8 @@ def load_lib():
     lib.websocketframeGpuLastError.argtypes = []
     lib.websocketframeGpuSetOption.restype = i32
     lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
+    lib.websocketframeGpuGetStat.restype = i32
+    lib.websocketframeGpuGetStat.argtypes = [C.c_char_p, P(C.c_ulonglong)]
     lib.websocketframeGpuCalibrate.restype = i32
     lib.websocketframeGpuCalibrate.argtypes = [vp, vp, u64, i32, i32, i32, vp]
     lib.websocketframeSynthDevice.restype = i32

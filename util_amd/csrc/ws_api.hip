@@ -26,6 +26,8 @@ extern int ws_encode_fused;
 extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_reasm_merge;
+extern int ws_stream_rw;
+extern unsigned long long ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -74,6 +76,15 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
+    else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
+    else return -1;
+    return 0;
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value) {
+    if (!value) return -1;
+    if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks;
+    else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks;
     else return -1;
     return 0;
 }

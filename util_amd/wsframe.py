@@ -212,3 +212,11 @@ def set_option(name, value):
     rc = load_lib().websocketframeGpuSetOption(name.encode(), int(value))
     if rc != 0:
         raise ValueError("unknown option %r" % name)
+
+
+def get_stat(name):
+    """websocketframeGpuGetStat (diagnostic counters of the most recent call)"""
+    v = C.c_ulonglong(0)
+    if load_lib().websocketframeGpuGetStat(name.encode(), C.byref(v)) != 0:
+        raise ValueError("unknown stat %r" % name)
+    return int(v.value)
