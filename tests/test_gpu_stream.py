@@ -114,13 +114,13 @@ def serial_walk():
 
 @pytest.mark.parametrize("shift", [0, 3])
 def test_long_stream_cfg3_mix(dev, shift):
-    """the cfg3 length mix as one 48 MiB client stream (4 MiB chunks)"""
+    """the cfg3 length mix as one 48 MiB client stream (16 MiB chunks)"""
     wire = long_stream(np.random.default_rng(21), 48 << 20, mix3, masked=1.0)
     r = run(dev, wire, 1 << 16, shift)
     assert int(r["consumed"]) == len(wire) and int(r["status"]) == W.SEG_OK
     # every chunk from the speculative records (no one-wavefront chunk walks; an unmasked
     # frame in a client stream would end its chunk's speculation)
-    assert W.get_stat("stream_rw_chunks") >= 11 and W.get_stat("stream_rw_chunk_walks") == 0
+    assert W.get_stat("stream_rw_chunks") >= 3 and W.get_stat("stream_rw_chunk_walks") == 0
 
 
 def test_long_stream_small_frames(dev):

@@ -26,7 +26,7 @@ extern int ws_encode_fused;
 extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_reasm_merge;
-extern int ws_stream_rw;
+extern int ws_stream_rw, ws_stream_rw_cmax;
 extern unsigned long long ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
 int ws_set_err(const char* what, hipError_t e) {
@@ -77,6 +77,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
+    else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
     else return -1;
     return 0;
 }

@@ -15,6 +15,8 @@
 // paying (a pass confirms fewer than 64 frames), the rest of the stream is walked by one
 // wavefront in a single launch (ws_stream_walk_kernel: stride speculation over 64
 // lanes, no host round trips) — lengths that change every frame are a serial chain.
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 //      (stream_walk from the chain's frame index), the last one also the tail, count and
 //      result.
 // Every byte decision is made by the reference rules; speculation only picks where to start.
-#define RW_CMAX (4ull << 20)
+#define RW_CMAX (16ull << 20)
 #define RW_CMIN (64ull << 10)
 #define RW_HMAX (128u << 10)
 #define RW_HMIN (4u << 10)
@@ -229,12 +231,23 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_S1 8           // ... of walks that end the stream in it
 #define RW_SLOTS (RW_S0 + RW_S1)
 #define RW_SLAST 4096     // walks that end the stream in the last chunk
-#define RW_MAXSTEPS 4096
+#define RW_MAXSTEPS 65536
+#define RW_TPOS 64        // window positions per thread
+#define RW_D 4            // distinct window exits per chunk walked on (phase B owners)
+#define RW_STG 4096       // staged frame offsets per owner
 
-struct RwRec {            // one surviving walk from chunk start + start
+struct RwRec {            // phase A: one surviving walk from chunk start + start
     u32 start;
-    u32 cs;               // frames consumed | status << 31 (0 left the chunk, 1 the stream's walk ends)
+    u32 cs;               // frames consumed | status << 31 (0 left the window, 1 the stream's walk ends)
     u64 exit;             // the next frame start (status 0) or where the walk ended
+};
+
+struct RwOwn {            // phase B: the walk from a window exit to the chunk's end
+    u64 exit;             // the next frame start (left the chunk) or where the stream's walk ends
+    u32 cs;               // frames | status << 31
+    u32 dead;             // 1: an implausible header (not the chain)
+    u64 over;             // the (RW_STG+1)-th frame's start when more than RW_STG frames
+    u64 pad;
 };
 
 // b23: header bytes 2 and 3 (the top of a 64-bit length, which a real frame leaves zero:
@@ -245,83 +258,209 @@ __device__ __forceinline__ bool rw_plausible(u32 b0, u32 b1, u32 b23, bool need_
            ((b1 & 0x7Fu) != 127u || b23 == 0u);
 }
 
-// one thread per 16 window positions (aligned loads); walks its plausible positions
-__global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
+// One speculative step at pos: 0 frame (pos advanced), 1 the stream's walk ends at pos,
+// 2 implausible header (a wrong start)
+__device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool need_mask) {
+    if (pos >= len || len - pos < 2) return 1;                               // websocketframe.c:121
+    const uintptr_t pa = origin + pos;
+    const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+    u64 h0, h1;
+    ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+    if (!rw_plausible((u32)h0 & 0xFFu, (u32)(h0 >> 8) & 0xFFu, (u32)(h0 >> 16) & 0xFFFFu, need_mask)) return 2;
+    const WsHdr h = ws_parse(h0, h1, len - pos);
+    if (h.kind != WS_PARSE_FRAME || h.ret <= 0) return 1;
+    pos += (u32)h.ret;
+    return 0;
+}
+
+// R1 (candidates): one thread per RW_TPOS window positions (aligned 16-B loads); the
+// plausible positions of a wavefront are appended to its chunk's list (capc slots) with
+// one atomic per wave on the chunk's counter
+// (lanes are dense in R2: a wrong start costs one lane-slot, not a wavefront-slot)
+__global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
-                                                         RwRec* __restrict__ recs, u32* __restrict__ nrec) {
+                                                         u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc) {
     const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
-    const u32 per = H / 16;
-    const u64 c = t / per;
+    const u32 lane = threadIdx.x & 63;
+    const u32 per = H / RW_TPOS;                                             // a multiple of 64: one
+    const u64 c = t / per;                                                   // chunk per wavefront
     if (c >= nchunks) return;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
-    const u64 cs0 = P + c * C, cend = cs0 + C;
-    const uintptr_t a = ((origin + cs0) & ~(uintptr_t)15) + (t % per) * 16;
-    if (a >= origin + len) return;                                           // reads stay within len + pad
-    const u32x4 x0 = reinterpret_cast<const gu32x4*>(a)[0], x1 = reinterpret_cast<const gu32x4*>(a)[1];
-    const u32 w[5] = {x0.x, x0.y, x0.z, x0.w, x1.x};
-    u32 cands = 0;
+    const u64 cs0 = P + c * C;
+    const uintptr_t a = ((origin + cs0) & ~(uintptr_t)15) + (t % per) * RW_TPOS;
+    u64 cands = 0;
+    if (a < origin + len) {
 #pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-        const u32 b0 = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-        const u32 b1 = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
-        const u32 b2 = (w[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xFFu;
-        const u32 b3 = (w[(k + 3) >> 2] >> (8 * ((k + 3) & 3))) & 0xFFu;
-        cands |= (rw_plausible(b0, b1, b2 | b3, need_mask) ? 1u : 0u) << k;
-    }
-    while (cands) {
-        const u32 k = (u32)__builtin_ctz(cands);
-        cands &= cands - 1;
-        const u64 start = a + k - origin;
-        if (start < cs0 || start >= len) continue;
-        u64 pos = start;
-        u32 cnt = 0, st = 0;
-        bool alive = true;
-        for (u32 step = 0;; ++step) {
-            if (pos >= cend) break;                                          // left the chunk
-            if (step >= RW_MAXSTEPS) { alive = false; break; }
-            if (pos >= len || len - pos < 2) { st = 1; break; }              // websocketframe.c:121
-            const uintptr_t pa = origin + pos;
-            const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-            u64 h0, h1;
-            ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
-            if (!rw_plausible((u32)h0 & 0xFFu, (u32)(h0 >> 8) & 0xFFu, (u32)(h0 >> 16) & 0xFFFFu, need_mask)) {
-                alive = false;
-                break;
+        for (u32 j = 0; j < RW_TPOS / 16; ++j) {
+            if (a + 16 * j >= origin + len) break;                           // reads stay within len + pad
+            const u32x4 x0 = reinterpret_cast<const gu32x4*>(a)[j], x1 = reinterpret_cast<const gu32x4*>(a)[j + 1];
+            const u32 w[5] = {x0.x, x0.y, x0.z, x0.w, x1.x};
+#pragma unroll
+            for (u32 k = 0; k < 16; ++k) {
+                const u32 b0 = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                const u32 b1 = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+                const u32 b2 = (w[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xFFu;
+                const u32 b3 = (w[(k + 3) >> 2] >> (8 * ((k + 3) & 3))) & 0xFFu;
+                const u64 pos = a + 16 * j + k - origin;
+                const bool ok = pos >= cs0 && pos < len && rw_plausible(b0, b1, b2 | b3, need_mask);
+                cands |= (u64)(ok ? 1u : 0u) << (16 * j + k);
             }
-            const WsHdr h = ws_parse(h0, h1, len - pos);
-            if (h.kind != WS_PARSE_FRAME || h.ret <= 0) { st = 1; break; }  // the stream's walk ends here
-            pos += (u32)h.ret;
-            ++cnt;
         }
-        if (!alive) continue;
-        // the last chunk's window lies near the stream's end, where wrong starts read as
-        // incomplete frames: its walks that end get a pool of their own
-        const bool lastc = c + 1 == nchunks;
-        const u32 slot = atomicAdd(nrec + 2 * c + st, 1u);
-        if (slot >= (st ? (lastc ? RW_SLAST : RW_S1) : RW_S0)) continue;
-        RwRec r;
-        r.start = (u32)(start - cs0);
-        r.cs = cnt | (st << 31);
-        r.exit = pos;
-        recs[st && lastc ? (u64)nchunks * RW_SLOTS + slot : c * RW_SLOTS + (st ? RW_S0 : 0) + slot] = r;
+    }
+    const u32 n = (u32)__builtin_popcountll(cands);
+    u32 incl = n;                                                            // wavefront inclusive scan
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+        const u32 v = (u32)__shfl_up((int)incl, d);
+        if (lane >= d) incl += v;
+    }
+    const u32 total = (u32)__shfl((int)incl, 63);
+    u32 base = 0;
+    if (lane == 63 && total) base = atomicAdd(nrec + 4 * c + 2, total);    // the chunk's counter
+    base = (u32)__shfl((int)base, 63);
+    u32 o = base + incl - n;
+    u64* cl = cand + c * capc;
+    while (cands) {
+        const u32 k = (u32)__builtin_ctzll(cands);
+        cands &= cands - 1;
+        if (o < capc) cl[o] = a + k - origin;
+        ++o;
     }
 }
 
-// emit: one wavefront per chain chunk: tab[b] = {entry, end, nf0, last}
+// R2 (window walks): one lane per candidate (grid-stride), the walk to the window's end
+// -> an A record {start, frames, exit_w}; a walk that left the window claims exit_w in
+// dx[] (one walk per distinct exit: merged walks share it) for R3
+__global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
+                                                         u64 C, u32 H, u32 nchunks, u32 need_mask,
+                                                         const u64* __restrict__ cand, u32 capc,
+                                                         RwRec* __restrict__ recs, u32* __restrict__ nrec,
+                                                         unsigned long long* __restrict__ dx) {
+    const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
+    const u64 n = (u64)nchunks * capc;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
+        const u64 c = i / capc;
+        if (i - c * capc >= nrec[4 * c + 2]) continue;                      // past the chunk's candidates
+        const u64 start = cand[i];
+        const u64 cs0 = P + c * C, cend = cs0 + C, wend = cs0 + H;
+        u64 pos = start;
+        u32 cnt = 0, r = 0;
+        while (pos < wend && (r = rw_step(origin, len, pos, need_mask)) == 0) ++cnt;
+        if (r == 2) continue;                                                // a wrong start
+        if (r == 0) {
+            // a wrong start just before the window's end crosses it in one jump: a few more
+            // plausible headers past it before the walk may claim its exit
+            u64 vp = pos;
+            u32 vr = 0;
+            for (u32 v = 0; v < 3 && vp < cend && (vr = rw_step(origin, len, vp, need_mask)) == 0; ++v) {
+            }
+            if (vr == 2) continue;
+        }
+        const u32 st = r;                                                    // 1: the walk ends in the window
+        // the last chunk's window lies near the stream's end, where wrong starts read as
+        // incomplete frames: its walks that end get a pool of their own
+        const bool lastc = c + 1 == nchunks;
+        const u32 slot = atomicAdd(nrec + 4 * c + st, 1u);
+        if (slot < (st ? (lastc ? RW_SLAST : RW_S1) : RW_S0)) {
+            RwRec rr;
+            rr.start = (u32)(start - cs0);
+            rr.cs = cnt | (st << 31);
+            rr.exit = pos;
+            recs[st && lastc ? (u64)nchunks * RW_SLOTS + slot : c * RW_SLOTS + (st ? RW_S0 : 0) + slot] = rr;
+        }
+        if (st) continue;
+        for (u32 d = 0; d < RW_D; ++d) {
+            const unsigned long long old = atomicCAS(dx + c * RW_D + d, 0ull, (unsigned long long)pos);
+            if (old == 0ull || old == pos) break;
+        }
+    }
+}
+
+// R3 (chunk walks): one lane per claimed window exit, the walk to the chunk's end; the
+// offsets of the frames it passes go to the staging list (the emit writes them in parallel)
+__global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
+                                                        u32 nchunks, u32 need_mask,
+                                                        const unsigned long long* __restrict__ dx,
+                                                        RwOwn* __restrict__ own, u32* __restrict__ stg) {
+    const u64 oi = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (oi >= (u64)nchunks * RW_D) return;
+    u64 pos = dx[oi];
+    if (!pos) return;
+    const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
+    const u64 c = oi / RW_D, cs0 = P + c * C, cend = cs0 + C;
+    u32* sl = stg + oi * RW_STG;
+    u32 nb = 0, r = 0;
+    u64 over = 0;
+    while (pos < cend) {
+        if (nb < RW_STG) sl[nb] = (u32)(pos - cs0);
+        else if (nb == RW_STG) over = pos;
+        if ((r = rw_step(origin, len, pos, need_mask)) != 0) break;
+        ++nb;
+        if (nb > RW_MAXSTEPS) { r = 2; break; }
+    }
+    RwOwn ow;
+    ow.exit = pos;
+    ow.cs = nb | ((r == 1 ? 1u : 0u) << 31);
+    ow.dead = r == 2 ? 1u : 0u;
+    ow.over = over;
+    ow.pad = 0;
+    own[oi] = ow;
+}
+
+// emit: one wavefront per chain chunk, tab[b] = {entry, exit_w, nf0, cnt_w, owner, n_par,
+// last, cs0}: the window prefix [entry, exit_w) by the group walk, then n_par staged
+// frames in parallel (lane i: frame i, i + 64, ...), then the group walk from the next
+// frame to the chunk's exit (or, last, to the stream's end: tail, count, result).
+// owner == ~0: the whole rest from entry by the group walk (a chain ending in the window).
 __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __restrict__ buf, u64 len, u32 max_frames,
-                                                        const u64* __restrict__ tab,
+                                                        const u64* __restrict__ tab, const RwOwn* __restrict__ own,
+                                                        const u32* __restrict__ stg,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
-    const u64* t = tab + 4 * blockIdx.x;
-    stream_walk(buf, len, t[0], 0, (u32)t[2], t[1], t[3] != 0, max_frames, desc, items, ptr, pend, nwork, res,
-                threadIdx.x);
+    const u64* t = tab + 8 * blockIdx.x;
+    const u64 ent = t[0], exit_w = t[1], nf0 = t[2], cnt_w = t[3], oi = t[4], n_par = t[5], cs0 = t[7];
+    const bool last = t[6] != 0;
+    const u32 lane = threadIdx.x;
+    if (oi == ~0ull) {
+        stream_walk(buf, len, ent, 0, (u32)nf0, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
+        return;
+    }
+    stream_walk(buf, len, ent, 0, (u32)nf0, exit_w, false, max_frames, desc, items, ptr, pend, nwork, res, lane);
+    const RwOwn ow = own[oi];
+    const u32* sl = stg + oi * RW_STG;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
+    for (u64 i = lane; i < n_par; i += 64) {
+        const u64 pos = cs0 + sl[i];
+        const uintptr_t pa = origin + pos;
+        const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+        u64 h0, h1;
+        ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+        const WsHdr h = ws_parse(h0, h1, len - pos);                         // a frame (the owner walked it)
+        const u64 slot = nf0 + cnt_w + i;
+        const u64 fo = lead0 + pos, p0 = fo + h.hdr, fe = p0 + h.plen;
+        const u64 w0 = p0 | ((u64)(rotl32(h.key, 8u * (u32)(p0 & 3)) & 0xFFFFu) << 48);
+        const u64 w1 = (h.masked ? fe : p0) | ((u64)(rotl32(h.key, 8u * (u32)(p0 & 3)) >> 16) << 48);
+        u32x4 it;
+        it.x = (u32)w0; it.y = (u32)(w0 >> 32); it.z = (u32)w1; it.w = (u32)(w1 >> 32);
+        *gptr<u32x4>(items + slot) = it;
+        for (u64 p = (fo + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S; (p << PIECE_SHIFT_S) < fe && p < pend; ++p)
+            *gptr<u64>(ptr + p) = slot;
+        ws_store_desc(desc + slot, pos, h);
+    }
+    const u64 nb = ow.cs & 0x7FFFFFFFu;
+    const u64 staged = nb < RW_STG ? nb : RW_STG;
+    const u64 next = n_par < staged ? cs0 + sl[n_par] : (n_par == nb ? ow.exit : ow.over);
+    stream_walk(buf, len, next, 0, (u32)(nf0 + cnt_w + n_par), last ? len : ow.exit, last, max_frames, desc, items,
+                ptr, pend, nwork, res, lane);
 }
 
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
 
 #define RW_MIN (16ull << 20)      // streams shorter than this after the passes: one wavefront walks
 int ws_stream_rw = 1;            // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
+int ws_stream_rw_cmax = 23;      // "stream_rw_cmax": log2 of the largest chunk
 extern int ws_dbg_flags;
 unsigned long long ws_stat_rw_chunks = 0;       // chunks written from records (last call)
 unsigned long long ws_stat_rw_chunk_walks = 0;  // chunks walked by one wavefront without a record
@@ -376,24 +515,12 @@ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
 static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames, WebsocketFrameDesc_t* d_desc,
                    const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st) {
     hipError_t e;
-    const u64 nchunks_max = (len - P + RW_CMIN - 1) / RW_CMIN;
-    const size_t b_recs = ((size_t)(nchunks_max * RW_SLOTS + RW_SLAST) * sizeof(RwRec) + 255) & ~(size_t)255;
-    const size_t b_nrec = ((size_t)nchunks_max * 8 + 255) & ~(size_t)255;
-    const size_t b_tab = ((size_t)nchunks_max * 32 + 255) & ~(size_t)255;
-    RwScratch* S = nullptr;
-    int rc = rw_scratch(b_recs + b_nrec + b_tab + 256, b_recs + b_nrec + 256, st, &S);
-    if (rc) return rc;
-    unsigned char* w = reinterpret_cast<unsigned char*>(S->d);
-    RwRec* recs = reinterpret_cast<RwRec*>(w);
-    u32* nrec = reinterpret_cast<u32*>(w + b_recs);
-    u64* tab = reinterpret_cast<u64*>(w + b_recs + b_nrec);
-    u64* wout = reinterpret_cast<u64*>(w + b_recs + b_nrec + b_tab);
-    unsigned char* hw = reinterpret_cast<unsigned char*>(S->h);
-    RwRec* hr = reinterpret_cast<RwRec*>(hw);
-    u32* hn = reinterpret_cast<u32*>(hw + b_recs);
-    u64* ho = reinterpret_cast<u64*>(hw + b_recs + b_nrec);                // chunk-walk reports, header bytes
+    int rc;
     ws_stat_rw_chunk_walks = 0;
     ws_stat_rw_chunks = 0;
+    RwScratch* S = nullptr;
+    u64* wout = nullptr;       // chunk-walk report (device) and its pinned copy
+    u64* ho = nullptr;
     // one chunk [ent, end) by one wavefront: the next entry, or the stream finished
     auto chunk_walk = [&](u64 ent, u32 nfc, u64 end, u64& next, u32& nfn) -> int {
         ++ws_stat_rw_chunk_walks;
@@ -409,6 +536,9 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         return ho[2] ? 1 : 0;
     };
     // sample: the first RW_SAMPLE bytes, and the mean wire length
+    if ((rc = rw_scratch(256, 256, st, &S))) return rc;
+    wout = reinterpret_cast<u64*>(S->d);
+    ho = reinterpret_cast<u64*>(S->h);
     u64 P1 = 0;
     u32 nf1 = 0;
     if ((rc = chunk_walk(P, nf, P + RW_SAMPLE, P1, nf1))) return rc < 0 ? rc : 0;
@@ -416,63 +546,115 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const u64 mean = nf1 > nf ? (P1 - P) / (nf1 - nf) : (P1 - P);
     P = P1;
     nf = nf1;
-    const u64 C = rw_pow2_clamp(mean * 512, RW_CMIN, RW_CMAX);
+    const u64 cmax = ws_stream_rw_cmax >= 16 && ws_stream_rw_cmax <= 26 ? 1ull << ws_stream_rw_cmax : RW_CMAX;
+    const u64 C = rw_pow2_clamp(mean * 1024, RW_CMIN, cmax);
     const u32 H = (u32)rw_pow2_clamp(mean * 8, RW_HMIN, C / 2 < RW_HMAX ? C / 2 : RW_HMAX);
     const u64 nchunks = (len - P + C - 1) / C;
+    const size_t b_recs = ((size_t)(nchunks * RW_SLOTS + RW_SLAST) * sizeof(RwRec) + 255) & ~(size_t)255;
+    const size_t b_nrec = ((size_t)nchunks * 16 + 255) & ~(size_t)255;     // per chunk: n0, n1, candidates
+    const size_t b_dx = ((size_t)nchunks * RW_D * 8 + 255) & ~(size_t)255;
+    const size_t b_own = ((size_t)nchunks * RW_D * sizeof(RwOwn) + 255) & ~(size_t)255;
+    const size_t b_tab = ((size_t)nchunks * 64 + 255) & ~(size_t)255;
+    const size_t b_stg = (size_t)nchunks * RW_D * RW_STG * 4;
+    const u32 capc = H / 32;                                                 // candidates: 1/32 of a window
+    const size_t b_cand = (size_t)nchunks * capc * 8;
+    const size_t b_host = b_recs + b_nrec + b_dx + 256 + b_own;              // copied back
+    if ((rc = rw_scratch(256 + b_host + b_tab + b_stg + b_cand, 256 + b_host, st, &S))) return rc;
+    unsigned char* w = reinterpret_cast<unsigned char*>(S->d);
+    unsigned char* hw = reinterpret_cast<unsigned char*>(S->h);
+    wout = reinterpret_cast<u64*>(w);
+    ho = reinterpret_cast<u64*>(hw);
+    RwRec* recs = reinterpret_cast<RwRec*>(w + 256);
+    u32* nrec = reinterpret_cast<u32*>(w + 256 + b_recs);
+    unsigned long long* dx = reinterpret_cast<unsigned long long*>(w + 256 + b_recs + b_nrec);
+    RwOwn* own = reinterpret_cast<RwOwn*>(w + 256 + b_recs + b_nrec + b_dx + 256);
+    u64* tab = reinterpret_cast<u64*>(w + 256 + b_host);
+    u32* stg = reinterpret_cast<u32*>(w + 256 + b_host + b_tab);
+    u64* cand = reinterpret_cast<u64*>(w + 256 + b_host + b_tab + b_stg);
+    const RwRec* hr = reinterpret_cast<const RwRec*>(hw + 256);
+    const u32* hn = reinterpret_cast<const u32*>(hw + 256 + b_recs);
+    const u64* hdx = reinterpret_cast<const u64*>(hw + 256 + b_recs + b_nrec);
+    const RwOwn* hown = reinterpret_cast<const RwOwn*>(hw + 256 + b_recs + b_nrec + b_dx + 256);
     // the stream's frames are masked if the one at P is (client streams): candidates must be too
     unsigned char* hb = reinterpret_cast<unsigned char*>(ho + 4);
     hb[1] = 0;
     if ((e = hipMemcpyAsync(hb, d_buf + P, 2, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemsetAsync(nrec, 0, nchunks * 8, st)) != hipSuccess ||
+        (e = hipMemsetAsync(nrec, 0, b_nrec + b_dx + 256, st)) != hipSuccess ||  // counters, claimed exits
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return ws_set_err("stream walk setup", e);
     const u32 need_mask = (hb[1] & 0x80u) ? 1u : 0u;
-    const u64 threads = nchunks * (H / 16);
-    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
-                       (u32)nchunks, need_mask, recs, nrec);
+    const u64 threads = nchunks * (H / RW_TPOS);
+    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
+                       (u32)nchunks, need_mask, cand, nrec, capc);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_cand_kernel launch", e);
+    const u32 r2_blocks = (u32)std::min<u64>((nchunks * capc + 255) / 256, 4096);  // grid-stride
+    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
+                       need_mask, cand, capc, recs, nrec, dx);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
-    if ((e = hipMemcpyAsync(hn, nrec, nchunks * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(hr, recs, nchunks * RW_SLOTS * sizeof(RwRec), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(hr + nchunks * RW_SLOTS, recs + nchunks * RW_SLOTS,
-                            (size_t)RW_SLAST * sizeof(RwRec), hipMemcpyDeviceToHost, st)) !=
-            hipSuccess ||
+    if (!(ws_dbg_flags & 128)) {                                             // A/B: window walks only
+        hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
+                           P, C, (u32)nchunks, need_mask, dx, own, stg);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
+    }
+    if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return ws_set_err("stream walk records", e);
+    const auto t_rec = std::chrono::steady_clock::now();
     // follow the chain from P: exact, every record is the reference loop from its start
     std::vector<u64> ht;
     u64 ent = P;
     u32 nfc = nf;
+    ht.reserve(nchunks * 8 + 8);
     for (bool last = false; !last;) {
         const u64 c = (ent - P) / C, cs0 = P + c * C;
+        if (c + 3 < nchunks) {                                               // the chain is sequential:
+            const u64 cp = c + 3;                                            // hide the host's cache misses
+            __builtin_prefetch(hn + 4 * cp);
+            for (u32 k = 0; k < 4; ++k) __builtin_prefetch(hr + cp * RW_SLOTS + 4 * k);
+            __builtin_prefetch(hdx + cp * RW_D);
+            __builtin_prefetch(hown + cp * RW_D);
+            __builtin_prefetch(hown + cp * RW_D + 2);
+        }
         const RwRec* r = nullptr;
         if (c < nchunks && ent - cs0 < H) {
             const u32 so = (u32)(ent - cs0);
-            for (u32 k = 0; k < hn[2 * c] && k < RW_S0; ++k)
+            for (u32 k = 0; k < hn[4 * c] && k < RW_S0; ++k)
                 if (hr[c * RW_SLOTS + k].start == so) { r = &hr[c * RW_SLOTS + k]; break; }
             const bool lastc = c + 1 == nchunks;
             const RwRec* r1 = lastc ? hr + nchunks * RW_SLOTS : hr + c * RW_SLOTS + RW_S0;
-            for (u32 k = 0; !r && k < hn[2 * c + 1] && k < (lastc ? RW_SLAST : RW_S1); ++k)
+            for (u32 k = 0; !r && k < hn[4 * c + 1] && k < (lastc ? RW_SLAST : RW_S1); ++k)
                 if (r1[k].start == so) { r = &r1[k]; break; }
         }
-        if (r) {
-            const u32 cnt = r->cs & 0x7FFFFFFFu;
-            last = (r->cs >> 31) != 0 || r->exit >= len || (u64)nfc + cnt >= max_frames;
-            ht.push_back(ent);
-            ht.push_back(last ? len : r->exit);
-            ht.push_back(nfc);
-            ht.push_back(last ? 1 : 0);
-            nfc += cnt;
-            ent = r->exit;
+        const RwOwn* ow = nullptr;
+        u64 oi = ~0ull;
+        if (r && !(r->cs >> 31))
+            for (u32 d = 0; d < RW_D; ++d)
+                if (hdx[c * RW_D + d] == r->exit) {
+                    oi = c * RW_D + d;
+                    ow = hown[oi].dead ? nullptr : &hown[oi];
+                    break;
+                }
+        const u32 cnt_w = r ? (r->cs & 0x7FFFFFFFu) : 0u;
+        if (r && ((r->cs >> 31) || (u64)nfc + cnt_w >= max_frames)) {      // ends in the window: group walk
+            const u64 row[8] = {ent, 0, nfc, 0, ~0ull, 0, 1, cs0};
+            ht.insert(ht.end(), row, row + 8);
+            break;
+        }
+        if (ow) {
+            const u32 nb = ow->cs & 0x7FFFFFFFu;
+            last = (ow->cs >> 31) != 0 || ow->exit >= len || (u64)nfc + cnt_w + nb >= max_frames;
+            u64 n_par = nb < RW_STG ? nb : RW_STG;
+            if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
+            const u64 row[8] = {ent, r->exit, nfc, cnt_w, oi, n_par, last ? 1ull : 0ull, cs0};
+            ht.insert(ht.end(), row, row + 8);
+            nfc += cnt_w + nb;
+            ent = ow->exit;
             continue;
         }
-        if ((ws_dbg_flags & 16) && ws_stat_rw_chunk_walks < 6 && c < nchunks) {
-            fprintf(stderr, "rw: chunk %llu/%llu C %llu H %u entry +%llu n0 %u n1 %u:", (unsigned long long)c,
-                    (unsigned long long)nchunks, (unsigned long long)C, H, (unsigned long long)(ent - cs0),
-                    hn[2 * c], hn[2 * c + 1]);
-            for (u32 k = 0; k < hn[2 * c] && k < RW_S0; ++k)
-                fprintf(stderr, " [%u %u]", hr[c * RW_SLOTS + k].start, hr[c * RW_SLOTS + k].cs);
-            fprintf(stderr, "\n");
-        }
+        if ((ws_dbg_flags & 16) && ws_stat_rw_chunk_walks < 6 && c < nchunks)
+            fprintf(stderr, "rw: chunk %llu/%llu C %llu H %u entry +%llu n0 %u n1 %u A %d owner %d\n",
+                    (unsigned long long)c, (unsigned long long)nchunks, (unsigned long long)C, H,
+                    (unsigned long long)(ent - cs0), hn[4 * c], hn[4 * c + 1], r ? 1 : 0, oi != ~0ull ? 1 : 0);
         u64 nx = 0;
         u32 nfn = 0;
         if ((rc = chunk_walk(ent, nfc, cs0 + C, nx, nfn)) < 0) return rc;
@@ -480,13 +662,30 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         ent = nx;
         nfc = nfn;
     }
-    const u32 nb = (u32)(ht.size() / 4);
-    ws_stat_rw_chunks = nb;
-    if (nb) {
+    const u32 nblk = (u32)(ht.size() / 8);
+    if (ws_dbg_flags & 64)
+        fprintf(stderr, "rw: chain of %u chunks resolved in %.1f us\n", (unsigned)(ht.size() / 8),
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_rec).count());
+    ws_stat_rw_chunks = nblk;
+    if (ws_dbg_flags & 32) {
+        fprintf(stderr, "rw: len %llu P %llu C %llu H %u nchunks %llu\n", (unsigned long long)len,
+                (unsigned long long)P, (unsigned long long)C, H, (unsigned long long)nchunks);
+        for (u32 i = 0; i < nblk; ++i) {
+            const u64* t = ht.data() + 8 * i;
+            fprintf(stderr, "rw: row %u ent %llu exit_w %llu nf0 %llu cnt_w %llu oi %lld n_par %llu last %llu", i,
+                    (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2],
+                    (unsigned long long)t[3], (long long)t[4], (unsigned long long)t[5], (unsigned long long)t[6]);
+            if (t[4] != ~0ull)
+                fprintf(stderr, " own exit %llu cs %x dead %u", (unsigned long long)hown[t[4]].exit, hown[t[4]].cs,
+                        hown[t[4]].dead);
+            fprintf(stderr, "\n");
+        }
+    }
+    if (nblk) {
         if ((e = hipMemcpyAsync(tab, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stream chain)", e);
-        hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nb), dim3(64), 0, st, d_buf, len, max_frames, tab, d_desc,
-                           Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+        hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nblk), dim3(64), 0, st, d_buf, len, max_frames, tab, own, stg,
+                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_emit_kernel launch", e);
     }
     // `ht` is pageable host memory read by the copy above: complete it before returning
