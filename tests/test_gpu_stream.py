@@ -185,3 +185,14 @@ def test_long_stream_same_as_serial(dev, serial_walk):
     """the one-wavefront walk on a chunk-parallel-sized stream (the option's other side)"""
     wire = long_stream(np.random.default_rng(28), 17 << 20, mix3)
     run(dev, wire, 1 << 14)
+
+
+def test_long_stream_length_shift(dev):
+    """the sample sees 64 KiB frames, the rest are ~1 KiB: chunks sized for big frames
+    hold far more frames than their staging lists (the emit walks the excess)"""
+    rng = np.random.default_rng(29)
+    big = long_stream(rng, 2 << 20, lambda g: 65536, masked=1.0)
+    small = long_stream(rng, 38 << 20, lambda g: g.integers(500, 1500), masked=1.0)
+    wire = np.concatenate([big, small])
+    r = run(dev, wire, 1 << 16)
+    assert int(r["consumed"]) == len(wire) and int(r["n_frames"]) > 30000

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_MAXSTEPS 65536
 #define RW_TPOS 64        // window positions per thread
 #define RW_D 4            // distinct window exits per chunk walked on (phase B owners)
-#define RW_STG 4096       // staged frame offsets per owner
+#define RW_STG 4096       // largest staging list per owner (frame offsets); the call's is stgn
 
 struct RwRec {            // phase A: one surviving walk from chunk start + start
     u32 start;
@@ -246,7 +246,7 @@ struct RwOwn {            // phase B: the walk from a window exit to the chunk's
     u64 exit;             // the next frame start (left the chunk) or where the stream's walk ends
     u32 cs;               // frames | status << 31
     u32 dead;             // 1: an implausible header (not the chain)
-    u64 over;             // the (RW_STG+1)-th frame's start when more than RW_STG frames
+    u64 over;             // the (stgn+1)-th frame's start when more than stgn frames
     u64 pad;
 };
 
@@ -381,19 +381,19 @@ __global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __
 __global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
                                                         u32 nchunks, u32 need_mask,
                                                         const unsigned long long* __restrict__ dx,
-                                                        RwOwn* __restrict__ own, u32* __restrict__ stg) {
+                                                        RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn) {
     const u64 oi = (u64)blockIdx.x * 256 + threadIdx.x;
     if (oi >= (u64)nchunks * RW_D) return;
     u64 pos = dx[oi];
     if (!pos) return;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
     const u64 c = oi / RW_D, cs0 = P + c * C, cend = cs0 + C;
-    u32* sl = stg + oi * RW_STG;
+    u32* sl = stg + oi * stgn;
     u32 nb = 0, r = 0;
     u64 over = 0;
     while (pos < cend) {
-        if (nb < RW_STG) sl[nb] = (u32)(pos - cs0);
-        else if (nb == RW_STG) over = pos;
+        if (nb < stgn) sl[nb] = (u32)(pos - cs0);
+        else if (nb == stgn) over = pos;
         if ((r = rw_step(origin, len, pos, need_mask)) != 0) break;
         ++nb;
         if (nb > RW_MAXSTEPS) { r = 2; break; }
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __r
 // owner == ~0: the whole rest from entry by the group walk (a chain ending in the window).
 __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __restrict__ buf, u64 len, u32 max_frames,
                                                         const u64* __restrict__ tab, const RwOwn* __restrict__ own,
-                                                        const u32* __restrict__ stg,
+                                                        const u32* __restrict__ stg, u32 stgn,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
     }
     stream_walk(buf, len, ent, 0, (u32)nf0, exit_w, false, max_frames, desc, items, ptr, pend, nwork, res, lane);
     const RwOwn ow = own[oi];
-    const u32* sl = stg + oi * RW_STG;
+    const u32* sl = stg + oi * stgn;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
     for (u64 i = lane; i < n_par; i += 64) {
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
         ws_store_desc(desc + slot, pos, h);
     }
     const u64 nb = ow.cs & 0x7FFFFFFFu;
-    const u64 staged = nb < RW_STG ? nb : RW_STG;
+    const u64 staged = nb < stgn ? nb : stgn;
     const u64 next = n_par < staged ? cs0 + sl[n_par] : (n_par == nb ? ow.exit : ow.over);
     stream_walk(buf, len, next, 0, (u32)(nf0 + cnt_w + n_par), last ? len : ow.exit, last, max_frames, desc, items,
                 ptr, pend, nwork, res, lane);
@@ -555,7 +555,9 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const size_t b_dx = ((size_t)nchunks * RW_D * 8 + 255) & ~(size_t)255;
     const size_t b_own = ((size_t)nchunks * RW_D * sizeof(RwOwn) + 255) & ~(size_t)255;
     const size_t b_tab = ((size_t)nchunks * 64 + 255) & ~(size_t)255;
-    const size_t b_stg = (size_t)nchunks * RW_D * RW_STG * 4;
+    // staging: about twice the chunk's mean frame count (frames past it are walked by the emit)
+    const u32 stgn = (u32)rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_STG);
+    const size_t b_stg = (size_t)nchunks * RW_D * stgn * 4;
     const u32 capc = H / 32;                                                 // candidates: 1/32 of a window
     const size_t b_cand = (size_t)nchunks * capc * 8;
     const size_t b_host = b_recs + b_nrec + b_dx + 256 + b_own;              // copied back
@@ -593,7 +595,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
     if (!(ws_dbg_flags & 128)) {                                             // A/B: window walks only
         hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
-                           P, C, (u32)nchunks, need_mask, dx, own, stg);
+                           P, C, (u32)nchunks, need_mask, dx, own, stg, stgn);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     }
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -643,7 +645,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         if (ow) {
             const u32 nb = ow->cs & 0x7FFFFFFFu;
             last = (ow->cs >> 31) != 0 || ow->exit >= len || (u64)nfc + cnt_w + nb >= max_frames;
-            u64 n_par = nb < RW_STG ? nb : RW_STG;
+            u64 n_par = nb < stgn ? nb : stgn;
             if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
             const u64 row[8] = {ent, r->exit, nfc, cnt_w, oi, n_par, last ? 1ull : 0ull, cs0};
             ht.insert(ht.end(), row, row + 8);
@@ -684,7 +686,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     if (nblk) {
         if ((e = hipMemcpyAsync(tab, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stream chain)", e);
-        hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nblk), dim3(64), 0, st, d_buf, len, max_frames, tab, own, stg,
+        hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nblk), dim3(64), 0, st, d_buf, len, max_frames, tab, own, stg, stgn,
                            d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_emit_kernel launch", e);
     }
