@@ -573,6 +573,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
+    ap.add_argument("--scatter", action="store_true",
+                    help="N > 1: also time rank 0 sending its wire batch to every other rank (a NIC-attached "
+                         "rx buffer on one GPU; RCCL point-to-point over xGMI), reported separately")
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
     ap.add_argument("--fps", type=int, default=None, help="override frames per rx segment (experiments)")
     ap.add_argument("--plen", type=int, default=None, help="override the fixed payload length (experiments)")
@@ -666,7 +669,7 @@ def main():
                      "kernel": KERNELS[kpath], "algo_bytes_per_launch": wl.algo_bytes,
                      "timed": "HIP events at the two ends of the timed region on the calls' stream / steps: " +
                               STEP_KERNELS.get(kpath, KERNELS[kpath]),
-                     "per_kernel_ns": pmc[1].get("per_kernel_avg_ns") if pmc else None,
+                     "per_kernel_ns_profiled": pmc[1].get("per_kernel_avg_ns") if pmc else None,
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
         "cpu_baseline": None,
@@ -674,6 +677,15 @@ def main():
     }
     if sample is not None:
         out["cpu_baseline"] = cpu_baseline(sample, min(args.cpu_threads, os.cpu_count() or 1))
+    if args.scatter and world > 1:                                 # SURVEY §8e (1), outside the timed region
+        recv = None if rank == 0 else torch.empty(wl.wire_bytes, dtype=torch.uint8, device=dev)
+        dt = D.allreduce([D.scatter_from_root(wl.buf, recv, wl.wire_bytes)], op="max", device=dev)[0]
+        out["scatter"] = {"what": "rank 0 sends its wire batch to each other rank, point-to-point sends posted "
+                                  "together (RCCL over xGMI), not part of value",
+                          "backend": dist.get_backend(), "bytes_per_rank": wl.wire_bytes, "ms": round(dt * 1e3, 3),
+                          "GBps_per_link": round(wl.wire_bytes / dt / 1e9, 1),
+                          "GBps_total": round((world - 1) * wl.wire_bytes / dt / 1e9, 1)}
+        del recv
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

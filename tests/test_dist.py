@@ -74,3 +74,33 @@ def test_gloo_world2_matches_single_process():
         assert tot == [float(res["n_frames"].sum()), float(res["consumed"].sum()), 0.0]
         assert tmax == [2.0]
     assert sum(o[3] for o in out) == len(so)
+
+
+def _scatter_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wire = torch.from_numpy(_batch()[0])
+    n = wire.numel() - 5                                       # a prefix: only nbytes travel
+    recv = None if rank == 0 else torch.zeros(wire.numel(), dtype=torch.uint8)
+    dt = D.scatter_from_root(wire if rank == 0 else None, recv, n)
+    ok = True if rank == 0 else bool(torch.equal(recv[:n], wire[:n]) and int(recv[n:].sum()) == 0)
+    q.put((rank, ok, dt))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_gloo_world3_scatter_from_root():
+    """bench --scatter's exchange (rank 0's rx batch to every other rank) on gloo"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_scatter_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=150) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in ps)
+    assert all(ok and dt >= 0 for _, ok, dt in out)
