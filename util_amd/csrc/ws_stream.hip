@@ -28,13 +28,10 @@
 // outcome bits packed with the candidate index: k << 36 | code << 34 | stf << 32 | (u32)ret
 //   code 1: consumed, length != g   2: consumed, walk ends (ret <= 0)   3: not consumed
 //   stf (code 3): 0 OK, 1 MAX_FRAMES, 2 LEN_WRAP; (code 2): 0 ret == 0, 1 ret < 0
-__global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned char* __restrict__ buf, u64 len,
-                                                                 u64 P, u64 g, u32 nf, u32 max_frames, u64 K,
-                                                                 WebsocketFrameDesc_t* __restrict__ desc,
-                                                                 u32x4* __restrict__ items, u64* __restrict__ ptr,
-                                                                 u64 pend, unsigned long long* __restrict__ stop) {
-    const u64 k = (u64)blockIdx.x * SPASS_T + threadIdx.x;
-    if (k >= K) return;
+__device__ __forceinline__ void stream_pass_one(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 g, u32 nf,
+                                                u32 max_frames, u64 k, WebsocketFrameDesc_t* __restrict__ desc,
+                                                u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
+                                                unsigned long long* __restrict__ stop) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const u64 pos = P + k * g;
     u32 code = 0, stf = 0;
@@ -71,6 +68,42 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned 
         atomicMin(stop, word);
     }
 }
+
+// Candidates k in [k0, K), grid-stride. gate != nullptr: a pass launched right behind the
+// probe pass (same stream) that runs only if the probe confirmed all of its candidates.
+// g == 0: the stride is the length of the frame at P (every thread parses it; 0 when it
+// is not a complete frame with a positive return, then only candidate 0 exists), and
+// the candidate count is min(K, what fits the stream and max_frames); block 0 reports
+// {g, candidates} in gk.
+__global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned char* __restrict__ buf, u64 len,
+                                                                 u64 P, u64 g, u32 nf, u32 max_frames, u64 k0, u64 K,
+                                                                 WebsocketFrameDesc_t* __restrict__ desc,
+                                                                 u32x4* __restrict__ items, u64* __restrict__ ptr,
+                                                                 u64 pend, unsigned long long* __restrict__ stop,
+                                                                 const unsigned long long* __restrict__ gate,
+                                                                 u64* __restrict__ gk) {
+    if (gate && *gate != ~0ull) return;
+    if (g == 0) {
+        if (P < len && len - P >= 2) {
+            const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + P);
+            const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+            u64 h0, h1;
+            ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+            const WsHdr h = ws_parse(h0, h1, len - P);
+            if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
+        }
+        u64 kf = g ? (len - P) / g + 1 : 1;
+        if (kf > (u64)max_frames - nf + 1) kf = (u64)max_frames - nf + 1;
+        K = kf < K ? kf : K;
+        if (gk && blockIdx.x == 0 && threadIdx.x == 0) {
+            gk[0] = g;
+            gk[1] = K;
+        }
+    }
+    for (u64 k = k0 + (u64)blockIdx.x * SPASS_T + threadIdx.x; k < K; k += (u64)gridDim.x * SPASS_T)
+        stream_pass_one(buf, len, P, g, nf, max_frames, k, desc, items, ptr, pend, stop);
+}
+
 
 // Piece pointers [lo, hi) -> val. With lo_from_item / hi_from_item the bound is the
 // payload end (P1, origin-relative) of item `item` instead: the extent of a frame whose
@@ -712,7 +745,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     if (rc) return rc;
     unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
     unsigned long long* d_stop = reinterpret_cast<unsigned long long*>(w8 + ((pws + 63) & ~(size_t)63));
-    u64* d_seg = reinterpret_cast<u64*>(d_stop + 2);                        // [0] offset 0, [1] length
+    u64* d_seg = reinterpret_cast<u64*>(d_stop + 4);                        // [0] offset 0, [1] length
     const u64 seg[2] = {0, len};
     if ((e = hipMemcpyAsync(d_seg, seg, sizeof(seg), hipMemcpyHostToDevice, st)) != hipSuccess)
         return ws_set_err("hipMemcpyAsync(segment)", e);
@@ -748,21 +781,41 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     bool walked = false;
     bool probe = true;                       // after a length change: a short pass first (a stream
                                              // whose lengths keep changing never pays a full one)
+    // stop words [0] probe / single pass, [1] the gated rest; [2..3] the derived {g, K}
+    u64* d_gk = reinterpret_cast<u64*>(d_stop + 2);
+    auto pass = [&](u64 gp, u64 k0, u64 K, unsigned long long* stop, const unsigned long long* gate) -> int {
+        const u64 blocks = std::min<u64>((K - k0 + SPASS_T - 1) / SPASS_T, 8192);   // grid-stride beyond
+        hipLaunchKernelGGL(ws_stream_pass_kernel, dim3((u32)blocks), dim3(SPASS_T), 0, st, d_buf, (u64)len, P, gp, nf,
+                           max_frames, k0, K, d_desc, Pw.items, Pw.ptr, Pw.npieces, stop, gate, d_gk);
+        const hipError_t e2 = hipGetLastError();
+        return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
+    };
+    const u64 KMAX = 1ull << 26, PROBE_K = 1ull << 12;
     for (;;) {
-        const u64 remaining = len - P;
-        u64 K = g ? remaining / g + 1 : 1;                                   // candidates this pass
-        if (K > (u64)max_frames - nf + 1) K = (u64)max_frames - nf + 1;
-        if (K > (probe ? (1ull << 12) : (1ull << 26))) K = probe ? (1ull << 12) : (1ull << 26);
-        const unsigned long long none = ~0ull;
-        if ((e = hipMemcpyAsync(d_stop, &none, 8, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return ws_set_err("hipMemcpyAsync(stop)", e);
-        hipLaunchKernelGGL(ws_stream_pass_kernel, dim3((u32)((K + SPASS_T - 1) / SPASS_T)), dim3(SPASS_T), 0, st, d_buf,
-                           (u64)len, P, g, nf, max_frames, K, d_desc, Pw.items, Pw.ptr, Pw.npieces, d_stop);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_pass_kernel launch", e);
-        unsigned long long word = 0;
-        if ((e = hipMemcpyAsync(&word, d_stop, 8, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        if ((e = hipMemsetAsync(d_stop, 0xFF, 16, st)) != hipSuccess) return ws_set_err("hipMemsetAsync(stop)", e);
+        u64 K;
+        unsigned long long words[4] = {0, 0, 0, 0};
+        if (probe) {
+            // after a length change (and at the start): the stride is the length of the frame
+            // at P, derived on the device; a probe pass of PROBE_K candidates and right behind
+            // it (no host round trip) the rest, gated on the probe's stop word
+            if ((rc = pass(0, 0, PROBE_K, d_stop, nullptr)) || (rc = pass(0, PROBE_K, KMAX, d_stop + 1, d_stop)))
+                return rc;
+        } else {
+            K = g ? (len - P) / g + 1 : 1;                                   // candidates this pass
+            if (K > (u64)max_frames - nf + 1) K = (u64)max_frames - nf + 1;
+            if (K > KMAX) K = KMAX;
+            if ((rc = pass(g, 0, K, d_stop, nullptr))) return rc;
+        }
+        if ((e = hipMemcpyAsync(words, d_stop, probe ? 32 : 16, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stop D2H)", e);
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+        if (probe) {
+            g = words[2];
+            K = words[3];
+            if (words[0] == ~0ull && K <= PROBE_K) words[1] = ~0ull;         // no rest pass ran
+        }
+        const unsigned long long word = words[0] != ~0ull ? words[0] : words[1];   // candidates are ordered
         if (word == ~0ull) {                                                 // all K candidates were g-frames
             nf += (u32)K;
             P += K * g;
