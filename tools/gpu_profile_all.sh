@@ -8,4 +8,5 @@ bash tools/profile.sh gpurun_out/${R}_piece
 bash tools/profile.sh gpurun_out/${R}_segfuse_cfg5 --config cfg5
 bash tools/profile.sh gpurun_out/${R}_reasm_fused --op reasm --config cfg5
 bash tools/profile.sh gpurun_out/${R}_encode_cfg2 --op encode
-for d in piece segfuse_cfg5 reasm_fused encode_cfg2; do echo "== $d"; cat gpurun_out/${R}_$d/bench.json; done
+bash tools/profile.sh gpurun_out/${R}_stream_cfg3 --op stream --config cfg3
+for d in piece segfuse_cfg5 reasm_fused encode_cfg2 stream_cfg3; do echo "== $d"; cut -c1-300 gpurun_out/${R}_$d/bench.json; done
