@@ -196,3 +196,10 @@ def test_long_stream_length_shift(dev):
     wire = np.concatenate([big, small])
     r = run(dev, wire, 1 << 16)
     assert int(r["consumed"]) == len(wire) and int(r["n_frames"]) > 30000
+
+
+def test_stream_tiny_frames_medium(dev):
+    """2 MiB of 2..40 B frames (about 80 K frames): the chunk-parallel walk from 512 KiB on"""
+    wire = long_stream(np.random.default_rng(30), 2 << 20, lambda g: g.integers(0, 27), masked=1.0)
+    r = run(dev, wire, 1 << 17)
+    assert int(r["consumed"]) == len(wire)

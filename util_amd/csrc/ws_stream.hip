@@ -491,7 +491,8 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
 
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
 
-#define RW_MIN (16ull << 20)      // streams shorter than this after the passes: one wavefront walks
+#define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
+#define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
 int ws_stream_rw = 1;            // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
 int ws_stream_rw_cmax = 23;      // "stream_rw_cmax": log2 of the largest chunk
 extern int ws_dbg_flags;
@@ -579,6 +580,12 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const u64 mean = nf1 > nf ? (P1 - P) / (nf1 - nf) : (P1 - P);
     P = P1;
     nf = nf1;
+    if ((len - P) / (mean ? mean : 1) < RW_MIN_FRAMES) {                    // a short rest: one wavefront
+        hipLaunchKernelGGL(ws_stream_walk_kernel, dim3(1), dim3(64), 0, st, d_buf, len, P, (u64)0, nf, max_frames,
+                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_walk_kernel launch", e);
+        return 0;
+    }
     const u64 cmax = ws_stream_rw_cmax >= 16 && ws_stream_rw_cmax <= 26 ? 1ull << ws_stream_rw_cmax : RW_CMAX;
     const u64 C = rw_pow2_clamp(mean * 1024, RW_CMIN, cmax);
     const u32 H = (u32)rw_pow2_clamp(mean * 8, RW_HMIN, C / 2 < RW_HMAX ? C / 2 : RW_HMAX);
