@@ -29,3 +29,25 @@ def test_c_batch_host_program(tmp_path):
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("batch_host ok ")
     assert int(out.stdout.split()[-1]) > 5000
+
+
+def test_c_stream_device_program(tmp_path):
+    """tests/c/stream_dev.c: a 24 MiB client stream of changing frame lengths (the
+    chunk-parallel walk) through websocketframeStreamDecodeDevice from plain C with the HIP
+    runtime API, checked against the reference loop over websocketframeDecode"""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    util_amd.load_lib()
+    exe = str(tmp_path / "stream_dev")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                    "-I", os.path.join(REPO, "include"), "-I", os.path.join(rocm, "include"),
+                    os.path.join(REPO, "tests", "c", "stream_dev.c"), "-L", libdir, "-lwsframe_amd",
+                    "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath," + libdir,
+                    "-Wl,-rpath," + os.path.join(rocm, "lib"), "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("stream_dev ok ")
+    assert int(out.stdout.split()[-1]) > 1000
