@@ -573,6 +573,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
+    ap.add_argument("--graph", action="store_true",
+                    help="decode: capture one call into a HIP graph and replay it for every step")
     ap.add_argument("--scatter", action="store_true",
                     help="N > 1: also time rank 0 sending its wire batch to every other rank (a NIC-attached "
                          "rx buffer on one GPU; RCCL point-to-point over xGMI), reported separately")
@@ -623,7 +625,16 @@ def main():
     for _ in range(args.warmup):
         wl.decode()
     torch.cuda.synchronize()
-    elapsed, step_ms = timed_region(wl.decode, args.steps, world)
+    step = wl.decode
+    if args.graph:                    # the call is host-sync free once its workspace exists
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            wl.W.batch_decode_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res)
+
+        def step():
+            graph.replay()
+            wl.decodes += 1
+    elapsed, step_ms = timed_region(step, args.steps, world)
     kern_ms = np.array([step_ms])
     from util_amd import dist as D
     elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
@@ -658,7 +669,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
-        "config": {"workload": Workload.DESCRIPTION[args.config], "config": args.config,
+        "config": {"workload": Workload.DESCRIPTION[args.config], "config": args.config, "hip_graph": args.graph,
                    "frames_per_gpu": wl.nframes, "frames_per_segment": wl.fps, "segments_per_gpu": wl.nseg,
                    "wire_bytes_per_gpu": wl.wire_bytes, "payload_bytes_per_gpu": wl.payload_bytes,
                    "parallelism": "frame-range shards, %d independent GPU(s)" % world},

@@ -1,0 +1,67 @@
+"""The batch decode inside a captured HIP graph (torch.cuda.CUDAGraph): the call is
+asynchronous with no host synchronisation once its workspace exists, so a reactor loop
+can replay one captured decode per batch. Replay results vs the oracle (one replay) and
+the in-place XOR's involution (two replays restore the wire)."""
+import numpy as np
+import pytest
+
+import wsynth
+from oracle_lib import oracle_segments
+from test_gpu_parity import random_stream
+from util_amd import wsframe as W
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _batches():
+    rng = np.random.default_rng(41)
+    wire, so, sl = random_stream(rng, 600)                    # the piece path (mixed segments)
+    yield "random", wire, so, sl, 16
+    wire, off, pl, plain = wsynth.make_batch(16 * 2048, 0, 1024, 2, 42)   # cfg5 shape: segfuse
+    so = [int(off[i]) for i in range(0, 16 * 2048, 16)]
+    ends = so[1:] + [len(wire)]
+    yield "cfg5", wire, so, [e - s for s, e in zip(so, ends)], 16
+
+
+@pytest.mark.parametrize("case", ["random", "cfg5"])
+def test_batch_decode_graph_replay(dev, case):
+    name, wire, so, sl, mf = next(b for b in _batches() if b[0] == case)
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(wire).to(dev)
+    so_t = torch.tensor(so, dtype=torch.int64, device=dev)
+    sl_t = torch.tensor(sl, dtype=torch.int64, device=dev)
+    desc = torch.zeros(len(so) * mf * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
+    d[:n].copy_(src)
+    W.batch_decode_device(d, so_t, sl_t, mf, desc, res)      # eager call: workspace exists from here on
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        W.batch_decode_device(d, so_t, sl_t, mf, desc, res)
+    d[:n].copy_(src)
+    desc.zero_()
+    res.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, so, sl, mf)
+    gr = res.cpu().numpy().view(W.SEGRES_DTYPE)
+    gd = desc.cpu().numpy().view(W.DESC_DTYPE).reshape(len(so), mf)
+    assert np.array_equal(gr, orr)
+    for s in range(len(so)):
+        k = int(orr[s]["n_frames"])
+        assert np.array_equal(gd[s, :k], od.reshape(len(so), mf)[s, :k]), s
+    assert np.array_equal(d[:n].cpu().numpy(), ob)
+    g.replay()                                                # XOR again: the wire comes back
+    torch.cuda.synchronize()
+    assert torch.equal(d[:n], src)
