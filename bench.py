@@ -563,6 +563,60 @@ def cpu_baseline(sample, threads, min_seconds=1.0, op="decode", frames_per_segme
                       "%s" % (nseg * frames_per_segment, nseg, payload / 2**20, passes, threads, what)}
 
 
+def run_inflight(args, wl0, dev, world, rank):
+    """K independent batches of the same config in flight together, one HIP stream each
+    (websocketframeBatchDecodeDevice keeps one workspace per stream): batch i's walk can
+    run beside batch i-1's unmask, so the per-call fixed cost (K1's dependent walk, the
+    kernel boundary, K2's ramp-up and drain) overlaps other work. Same contract as the
+    main region: barrier + synchronize on both sides, events on the base stream at the
+    two ends only (every stream waits on the first and the base stream on every stream
+    before the second). Not part of `value`."""
+    import torch
+    import torch.distributed as dist
+    k = args.inflight
+    wls = [wl0] + [Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank + 7919 * i, fps=args.fps,
+                                 plen=args.plen) for i in range(1, k)]
+    streams = [torch.cuda.Stream(dev) for _ in range(k)]
+    base = torch.cuda.current_stream()
+    base.synchronize()
+    for i in range(max(args.warmup, 2 * k)):
+        wls[i % k].decode(stream=streams[i % k])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(base)
+    for s in streams:
+        s.wait_event(e0)
+    payload = 0
+    for i in range(args.steps):
+        wls[i % k].decode(stream=streams[i % k])
+        payload += wls[i % k].payload_bytes
+    for s in streams:
+        base.wait_stream(s)
+    e1.record(base)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    dev_ms = e0.elapsed_time(e1)
+    from util_amd import dist as D
+    wall = D.allreduce([wall], op="max", device=dev)[0]
+    mism = sum(w.verify(expect_plain=(w.decodes % 2 == 1)) for w in wls)
+    for w in wls[1:]:
+        w.free()
+    algo = sum(wls[i % k].algo_bytes for i in range(args.steps))
+    return {"batches_in_flight": k, "streams": k,
+            "value": round(payload * world / wall / 2**30, 2), "unit": "GiB/s",
+            "ms_per_batch": round(wall / args.steps * 1e3, 4),
+            "device_ms_per_batch": round(dev_ms / args.steps, 4),
+            "frac": round(algo / (dev_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+            "what": "K independent batches of this config, one HIP stream each, calls issued round-robin; "
+                    "not part of value", "verified": mism == 0}, mism
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -581,6 +635,10 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
     ap.add_argument("--fps", type=int, default=None, help="override frames per rx segment (experiments)")
     ap.add_argument("--plen", type=int, default=None, help="override the fixed payload length (experiments)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="decode: also time K independent batches of the config in flight together, one HIP "
+                         "stream each (a reactor with successive rx batches), reported as the 'inflight' field "
+                         "(1 = off)")
     ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm", "stream"],
                     help="decode (the headline), client-side encode + mask of the same frames, fused "
                          "decode + message reassembly (use with --config cfg5), or the whole batch as ONE raw "
@@ -648,6 +706,10 @@ def main():
         e2e_mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
         e2e["verified"] = e2e_mism == 0
         mism += e2e_mism
+    inflight = None
+    if args.inflight > 1:
+        inflight, m = run_inflight(args, wl, dev, world, rank)
+        mism += m
     mism = int(D.allreduce([mism], device=dev)[0])
 
     payload_all = wl.payload_bytes * world * args.steps
@@ -686,6 +748,8 @@ def main():
         "cpu_baseline": None,
         "e2e": e2e,
     }
+    if inflight is not None:
+        out["inflight"] = inflight
     if sample is not None:
         out["cpu_baseline"] = cpu_baseline(sample, min(args.cpu_threads, os.cpu_count() or 1))
     if args.scatter and world > 1:                                 # SURVEY §8e (1), outside the timed region

@@ -129,6 +129,11 @@ typedef struct WebsocketSegResult_t {
  *   off = 0; while (off < len) { r = websocketframeDecode(buf+off, len-off, ...);
  *                                if (r < 0) error; if (r == 0) break; off += r; }
  * (net_reactor.c:515-526), including every reference quirk (§SURVEY 4).
+ * Concurrency: every HIP stream (up to 16 per device) gets its own workspace, so calls
+ * on different streams — several rx batches in flight, one stream each, from one or
+ * several host threads — may overlap in time (batches must not share bytes). The first
+ * call on a stream (and a call on a larger batch) may allocate: make it before capturing
+ * calls into a HIP graph.
  * Returns 0, or a negative code if the launch failed (see websocketframeGpuLastError). */
 WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, unsigned long long buflen,
                                                        const unsigned long long* d_seg_off,

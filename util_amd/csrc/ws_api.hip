@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <deque>
+#include <mutex>
 
 #include "ws_common.h"
 
@@ -91,24 +93,32 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-device state: CU count, the walker's dequeue-counter ring, and the split
-// path's workspace (4-B key per descriptor slot + 4-B work count per segment),
-// grown on demand. Growing allocates, so size it once (a first call) before
-// capturing calls into a HIP graph. One workspace per device: concurrent calls
-// on different streams of one device must not overlap in time.
+// Per-device state: CU count, the walker's dequeue-counter ring, and one workspace set
+// (decode + encode) per HIP stream, grown on demand. Calls on different streams of one
+// device may overlap in time (a reactor with several rx batches in flight, one stream
+// each); calls on one stream are ordered by the stream (slot rules: stream_slot).
 #define WS_MAX_DEV 64
 #define WS_CTR_RING 64
+#define WS_STREAM_SLOTS 16
+struct WsStreamWs {
+    hipStream_t stream = nullptr;
+    bool captured = false;         // first used by a capturing stream: never reassigned
+    unsigned long long last = 0;   // LRU tick
+    u32* ws = nullptr;             // decode / reassembly / stream workspace
+    size_t ws_bytes = 0;
+    void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
+    size_t ews_bytes = 0;
+};
 struct WsDevState {
     int init = 0;
     int cus = 0;
     u32* ctr = nullptr;
-    unsigned slot = 0;
-    u32* ws = nullptr;
-    size_t ws_bytes = 0;
-    void* ews = nullptr;     // encode workspace (scan temp + piece pointers)
-    size_t ews_bytes = 0;
+    std::atomic<unsigned> slot{0};
+    std::deque<WsStreamWs> sw;     // grows; stable addresses
+    unsigned long long tick = 0;
 };
 static WsDevState g_dev[WS_MAX_DEV];
+static std::mutex g_dev_mu;        // device init and the stream-slot table
 
 static int dev_state(WsDevState** out) {
     int dev = 0;
@@ -116,6 +126,7 @@ static int dev_state(WsDevState** out) {
     if (e != hipSuccess) return ws_set_err("hipGetDevice", e);
     if (dev < 0 || dev >= WS_MAX_DEV) return ws_set_err("device index", hipErrorInvalidDevice);
     WsDevState& st = g_dev[dev];
+    std::lock_guard<std::mutex> lk(g_dev_mu);
     if (!st.init) {
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return ws_set_err("hipGetDeviceProperties", e);
@@ -128,19 +139,76 @@ static int dev_state(WsDevState** out) {
     return 0;
 }
 
-static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream) {
-    if (ds->ws_bytes >= bytes) return 0;
+static bool capturing(hipStream_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
+// the stream's workspace slot (caller holds g_dev_mu). Eager calls keep at most
+// WS_STREAM_SLOTS slots: a further stream takes the least recently used one after a
+// device synchronize. A stream capturing a graph cannot synchronize, so it always gets
+// a slot of its own (its graph keeps using that workspace on every replay).
+static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
+    WsStreamWs* lru = nullptr;
+    for (WsStreamWs& w : ds->sw) {
+        if (w.stream == stream) {
+            w.last = ++ds->tick;
+            *out = &w;
+            return 0;
+        }
+        if (!w.captured && (!lru || w.last < lru->last)) lru = &w;
+    }
+    const bool cap = capturing(stream);
+    if (cap || ds->sw.size() < WS_STREAM_SLOTS || !lru) {
+        ds->sw.emplace_back();
+        lru = &ds->sw.back();
+        lru->captured = cap;
+    } else {                       // every slot taken by another stream: drain the device, then reuse
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return ws_set_err("hipDeviceSynchronize", e);
+    }
+    lru->stream = stream;
+    lru->last = ++ds->tick;
+    *out = lru;
+    return 0;
+}
+
+// grow *p to at least `bytes` (the stream's previous work may still read it: drain first).
+// A stream capturing a graph (e.g. torch's private capture stream) may get its first
+// allocation (hipMalloc in relaxed capture mode, the head zeroed by a captured memset)
+// but cannot drain and free an existing one.
+static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, bool zero_head, const char* what) {
+    if (*have >= bytes) return 0;
     hipError_t e;
-    if (ds->ws) {
+    const bool cap = capturing(stream);
+    if (*p) {
+        if (cap) return ws_set_msg("workspace must grow while the stream captures a graph: "
+                                   "make one call of this size on the stream before capturing");
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
-        (void)hipFree(ds->ws);
-        ds->ws = nullptr;
-        ds->ws_bytes = 0;
+        (void)hipFree(*p);
+        *p = nullptr;
+        *have = 0;
     }
     const size_t sz = bytes + bytes / 4 + 4096;
-    if ((e = hipMalloc(&ds->ws, sz)) != hipSuccess) return ws_set_err("hipMalloc(workspace)", e);
-    if ((e = hipMemset(ds->ws, 0, 16)) != hipSuccess) return ws_set_err("hipMemset(workspace)", e);
-    ds->ws_bytes = sz;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
+    e = hipMalloc(p, sz);
+    if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (e != hipSuccess) return ws_set_err(what, e);
+    if (zero_head && (e = hipMemsetAsync(*p, 0, 16, stream)) != hipSuccess) return ws_set_err(what, e);
+    *have = sz;
+    return 0;
+}
+
+static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream, void** out) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    WsStreamWs* w = nullptr;
+    int rc = stream_slot(ds, stream, &w);
+    if (rc) return rc;
+    void* p = w->ws;
+    if ((rc = grow(&p, &w->ws_bytes, bytes, stream, true, "hipMalloc(workspace)"))) return rc;
+    w->ws = reinterpret_cast<u32*>(p);
+    *out = p;
     return 0;
 }
 
@@ -149,19 +217,11 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
-    hipError_t e;
-    if (ds->ews_bytes < bytes) {
-        if (ds->ews) {
-            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
-            (void)hipFree(ds->ews);
-            ds->ews = nullptr;
-            ds->ews_bytes = 0;
-        }
-        const size_t sz = bytes + bytes / 4 + 4096;
-        if ((e = hipMalloc(&ds->ews, sz)) != hipSuccess) return ws_set_err("hipMalloc(encode workspace)", e);
-        ds->ews_bytes = sz;
-    }
-    *out = ds->ews;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    WsStreamWs* w = nullptr;
+    if ((rc = stream_slot(ds, stream, &w))) return rc;
+    if ((rc = grow(&w->ews, &w->ews_bytes, bytes, stream, false, "hipMalloc(encode workspace)"))) return rc;
+    *out = w->ews;
     return 0;
 }
 
@@ -173,14 +233,12 @@ u32 ws_next_gen() {
     return gen;
 }
 
-// the per-device decode workspace (first 16 bytes zeroed at allocation)
+// the calling stream's decode workspace (first 16 bytes zeroed at allocation)
 int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
-    if ((rc = workspace(ds, bytes, stream))) return rc;
-    *out = ds->ws;
-    return 0;
+    return workspace(ds, bytes, stream, out);
 }
 
 // the decode variant a call takes
@@ -224,8 +282,7 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
     if (ws && ws_bytes < need) return ws_set_msg("websocketframe batch decode: workspace too small");
     if (!ws && need) {
-        if ((rc = workspace(ds, need, L.stream))) return rc;
-        ws = ds->ws;
+        if ((rc = workspace(ds, need, L.stream, &ws))) return rc;
     }
     if (path == 3) {
         const u32 gen = ws_next_gen();
