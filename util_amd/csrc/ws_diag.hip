@@ -160,6 +160,60 @@ __global__ __launch_bounds__(256) void ws_calib_rounds_kernel(gu32x4* __restrict
     }
 }
 
+// mode 70/71: persistent in-place XOR over 16 KiB pieces (4 loads + 4 stores per lane).
+// 70: work stealing — a block takes its next piece from a global ticket counter (drawn
+// while its loads are in flight), so CUs/XCDs that run faster take more pieces and the
+// grid drains together; 71: static, block b takes pieces b, b+G, ...
+template <bool STEAL>
+__global__ __launch_bounds__(256) void ws_calib_persist_kernel(gu32x4* __restrict__ a, u64 n, u32* __restrict__ ctr,
+                                                              u32 key) {
+    __shared__ u32 s_next[2];
+    const u64 npieces = (n + 1023) / 1024, last = n - 1;
+    u64 piece;
+    if (STEAL) {
+        if (threadIdx.x == 0) s_next[0] = atomicAdd(ctr, 1u);
+        __syncthreads();
+        piece = s_next[0];
+    } else {
+        piece = blockIdx.x;
+    }
+    u32 par = 1;
+#pragma unroll 1
+    while (piece < npieces) {
+        const u64 i = piece * 1024 + threadIdx.x;
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ld16<1>(a + min(i + 256u * u, last));
+        if (STEAL && threadIdx.x == 0) s_next[par] = atomicAdd(ctr, 1u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + 256u * u < n) st16<1>(v[u] ^ key, a + i + 256u * u);
+        if (STEAL) {
+            __syncthreads();
+            piece = s_next[par];
+            par ^= 1u;
+        } else {
+            piece += gridDim.x;
+        }
+    }
+}
+
+// mode 72: one-shot grid over 16 KiB pieces split into W windows streamed side by side
+// (block b takes piece (b % W) * ceil(P / W) + b / W)
+__global__ __launch_bounds__(256) void ws_calib_windows_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw,
+                                                              u32 key) {
+    const u64 npieces = (n + 1023) / 1024, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u64 i = piece * 1024 + threadIdx.x;
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld16<1>(a + min(i + 256u * u, last));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i + 256u * u < n) st16<1>(v[u] ^ key, a + i + 256u * u);
+}
+
 // mode 16+: one-shot in-place XOR through buffer instructions with explicit cache
 // bits (aux: bit0 sc0, bit1 nt, bit4 sc1), T threads x U chunks per block.
 template <int T, int U, int LAUX, int SAUX>
@@ -293,6 +347,23 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         else hipLaunchKernelGGL((ws_calib_oneshot_kernel<0>), dim3((u32)nb), dim3(256), 0, st, a, n, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_oneshot_kernel launch", e);
+    }
+    if (mode == 72) {  // `blocks` = number of windows
+        const u32 W = blocks > 0 ? (u32)blocks : 2u;
+        const u64 np = (n + 1023) / 1024, ppw = (np + W - 1) / W;
+        hipLaunchKernelGGL(ws_calib_windows_kernel, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_kernel launch", e);
+    }
+    if (mode == 70 || mode == 71) {  // persistent; d_b's first 4 bytes are the ticket counter
+        const u32 nb = blocks > 0 ? (u32)blocks : 2048u;
+        u32* ctr = reinterpret_cast<u32*>(d_b);
+        hipError_t e = hipMemsetAsync(ctr, 0, 4, st);
+        if (e != hipSuccess) return ws_set_err("hipMemsetAsync(calib counter)", e);
+        if (mode == 70) hipLaunchKernelGGL((ws_calib_persist_kernel<true>), dim3(nb), dim3(256), 0, st, a, n, ctr, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL((ws_calib_persist_kernel<false>), dim3(nb), dim3(256), 0, st, a, n, ctr, 0x5A5A5A5Au);
+        e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_persist_kernel launch", e);
     }
     if (mode >= 60) {  // one-shot + dependent lookups (d_b must hold >= 16 MiB)
         switch (mode) {

@@ -231,10 +231,17 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   const u32* __restrict__ disorder, u32 gen, u64 pbase,
                                                                   u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
-                                                                  WebsocketSegResult_t* __restrict__ res) {
+                                                                  WebsocketSegResult_t* __restrict__ res,
+                                                                  u32 wshift, u64 ppw, u64 npieces) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const u64 pc0 = (pbase + blockIdx.x) << (PIECE_SHIFT - 4);              // first chunk of the piece
+    // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
+    // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
+    // clamped piece and store nothing
+    const u64 pw = (u64)(blockIdx.x & ((1u << wshift) - 1u)) * ppw + (blockIdx.x >> wshift);
+    const bool pvalid = pw < npieces;
+    const u64 pidx = pvalid ? pw : npieces - 1;
+    const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
     const u64 wc0 = pc0 + (u64)wv * (64 * PIECE_U);                          // this wave's 4 KiB: 256 chunks
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
     // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
@@ -248,14 +255,14 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     constexpr long long RW = 64 * PIECE_U * 16;                             // this wave's bytes
     const u64 r0 = wc0 << 4, r1 = r0 + RW;
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-        reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
+        reinterpret_cast<uintptr_t>(ptr + pidx));
     const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
     u32 m[PIECE_U][4];
     u32 cov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) { m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0; cov[u] = 0; }
     // no early return: an exit branch here would be hoisted above the payload loads
-    u32 s = ok && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
+    u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
@@ -429,6 +436,8 @@ int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, 
 int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
 int ws_piece_occ = 0;     // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
+int ws_piece_win = 1;     // "piece_win": log2 of the number of piece windows K2 streams side by side
+                          // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
     if (!P.npieces) return 0;
@@ -440,9 +449,12 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
                                                                    : ws_piece_unmask_kernel<0, 0, 1>));
     if (ws_piece_occ == 7 || ws_piece_occ == 8)           // forced occupancy: spills, measured slower
         k = ws_piece_occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
-    hipLaunchKernelGGL(k, dim3((u32)P.npieces), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
+    u32 wshift = (u32)(ws_piece_win < 0 ? 0 : (ws_piece_win > 6 ? 6 : ws_piece_win));
+    while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
+    const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
+    hipLaunchKernelGGL(k, dim3((u32)(ppw << wshift)), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                        L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
-                       L.desc, L.res);
+                       L.desc, L.res, wshift, ppw, (u64)P.npieces);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
 }
