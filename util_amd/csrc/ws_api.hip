@@ -28,6 +28,7 @@ extern int ws_encode_fused;
 extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_piece_win;
+int ws_seg_win = 1;       // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern int ws_reasm_merge;
 extern int ws_stream_rw, ws_stream_rw_cmax;
 extern unsigned long long ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
@@ -79,6 +80,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
     else if (!strcmp(name, "piece_win")) ws_piece_win = (int)value;
+    else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
     else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;

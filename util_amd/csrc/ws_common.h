@@ -331,3 +331,9 @@ int ws_launch_split(const WsLaunch& L, int variant, int nt, u32* keys, u32* nwor
 int ws_launch_segblock(const WsLaunch& L, int cfg, int nt);
 int ws_launch_segfuse(const WsLaunch& L, int nt);
 bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
+
+// Block -> work item with the items split into two windows streamed side by side
+// (block b takes item (b & 1) * half + b / 2; half = 0 keeps b): two distant address
+// windows in flight beat one compact window on this HBM (tools/exp_win.sh).
+__device__ __forceinline__ u32 ws_win2(u32 b, u32 half) { return half ? (b & 1u) * half + (b >> 1) : b; }
+extern int ws_seg_win;

@@ -43,13 +43,14 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
                                                           const u64* __restrict__ seg_len, u32 max_frames,
                                                           const u64* __restrict__ desc_base,
                                                           WebsocketFrameDesc_t* __restrict__ desc,
-                                                          WebsocketSegResult_t* __restrict__ res) {
+                                                          WebsocketSegResult_t* __restrict__ res, u32 nseg, u32 half) {
     constexpr u32 SF_C = (SF_L - 1) * 64;             // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[SF_L * 64];
     __shared__ FrameL tab[SF_TB];
     __shared__ u64 sh_next;                         // next window's first chunk, ~0 = done
     __shared__ u32 sh_flo, sh_fhi;                  // frames with bytes in this window [flo, fhi)
-    const u32 s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const u32 s = ws_win2(blockIdx.x, half), tid = threadIdx.x, lane = tid & 63;
+    if (s >= nseg) return;                          // the odd grid's spare block
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 so = seg_off[s], sl = seg_len[s];
     const uintptr_t segp = reinterpret_cast<uintptr_t>(buf + so);
@@ -165,7 +166,8 @@ int ws_segfuse_cfg = 0;   // "segfuse_cfg": 0 256 threads, 17 KiB windows (8 wor
 
 int ws_launch_segfuse(const WsLaunch& L, int nt) {
     if (L.max_frames > SF_TB) return ws_set_msg("segfuse path: max_frames > 64");
-    void (*k)(unsigned char*, const u64*, const u64*, u32, const u64*, WebsocketFrameDesc_t*, WebsocketSegResult_t*);
+    void (*k)(unsigned char*, const u64*, const u64*, u32, const u64*, WebsocketFrameDesc_t*, WebsocketSegResult_t*,
+              u32, u32);
     int T = 256;
     switch (ws_segfuse_cfg) {
         case 1: k = nt == 1 ? ws_segfuse_kernel<1, 20, 256> : ws_segfuse_kernel<0, 20, 256>; break;
@@ -173,8 +175,9 @@ int ws_launch_segfuse(const WsLaunch& L, int nt) {
         case 3: k = nt == 1 ? ws_segfuse_kernel<1, 34, 512> : ws_segfuse_kernel<0, 34, 512>; T = 512; break;
         default: k = nt == 1 ? ws_segfuse_kernel<1, 18, 256> : ws_segfuse_kernel<0, 18, 256>;
     }
-    hipLaunchKernelGGL(k, dim3(L.nseg), dim3(T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.max_frames,
-                       L.desc_base, L.desc, L.res);
+    const u32 half = ws_seg_win && L.nseg >= 512 ? (L.nseg + 1) / 2 : 0;
+    hipLaunchKernelGGL(k, dim3(half ? 2 * half : L.nseg), dim3(T), 0, L.stream, L.buf, L.seg_off, L.seg_len,
+                       L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_segfuse_kernel launch", e);
 }
