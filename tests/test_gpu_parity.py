@@ -321,3 +321,24 @@ def test_int_truncation_real_size(dev, decode_path, total):
     else:
         assert int(gr[0]["n_frames"]) == 0 and int(gr[0]["consumed"]) == 0
     del gb, ob, host
+
+
+@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0)])
+def test_window_mappings(dev, decode_path, opt, val):
+    """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
+    blocks store nothing) and the segment kernels' two-window order (seg_win) at every
+    setting, on a batch large enough for every window to be used: bit-exact vs the oracle"""
+    W.set_option(opt, val)
+    try:
+        wire, off, pl, plain = wsynth.make_batch(2100, wsynth.PLEN_MIX3, 0, wsynth.B0_BINARY, 77)
+        wire = np.concatenate([wire, wire[:1000]])                   # + an incomplete tail
+        so = [int(off[i]) for i in range(0, 2100, 16)]
+        ends = so[1:] + [len(wire)]
+        assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d" % (opt, val))
+        wire, off, pl, plain = wsynth.make_batch(16 * 1100, 0, 1024, 2, 78)   # cfg5 shape (segfuse)
+        so = [int(off[i]) for i in range(0, 16 * 1100, 16)]
+        ends = so[1:] + [len(wire)]
+        assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d cfg5" % (opt, val))
+    finally:
+        W.set_option("piece_win", 1)
+        W.set_option("seg_win", 1)

@@ -169,16 +169,18 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
                                                             const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
                                                             const u64* __restrict__ wire_off,
                                                             const u32* __restrict__ ptr, unsigned char* __restrict__ dst,
-                                                            u64 capacity) {
+                                                            u64 capacity, u32 npieces, u32 half) {
     const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 pb = ws_win2(blockIdx.x, half);                                // output piece (two windows)
+    if (pb >= npieces) return;                                               // the odd grid's spare block
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
     const u64 total = min(wire_off[n], capacity);                            // never write past the capacity
     const u64 out_lo = lead0, out_hi = lead0 + total;                        // origin-relative output
-    const u64 r0 = (((u64)blockIdx.x << ENC_SHIFT) + (u64)wv * (64 * ENC_U * 16));  // origin-relative
+    const u64 r0 = (((u64)pb << ENC_SHIFT) + (u64)wv * (64 * ENC_U * 16));  // origin-relative
     const u64 r1 = r0 + 64 * ENC_U * 16;
-    const u32 first = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + blockIdx.x));
+    const u32 first = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + pb));
     if (first == ENC_NONE) return;
     // chunk state: fast = one payload source for the whole chunk
     u64 fsrc[ENC_U];
@@ -362,6 +364,7 @@ static int enc_side(EncSide** out) {
 }
 int ws_encode_fused = 0;  // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
                           // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
+int ws_enc_win = 0;       // "enc_win": E3 takes output pieces in two windows (ws_win2; measured 1 % slower)
 int ws_encode_side = 0;   // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
                           // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
@@ -404,8 +407,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     if (npieces) {
         auto copy = ws_encode_fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
-        hipLaunchKernelGGL(copy, dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes, d_wire_off, ptr,
-                           d_dst, (u64)dst_capacity);
+        const u32 half = ws_enc_win && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0;
+        hipLaunchKernelGGL(copy, dim3(half ? 2 * half : (u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
+                           d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, half);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
     if (S) {
