@@ -232,13 +232,16 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
                                                                   WebsocketSegResult_t* __restrict__ res,
-                                                                  u32 wshift, u64 ppw, u64 npieces) {
+                                                                  u32 wshift, u32 wbit, u64 ppw, u64 npieces) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
-    const u64 pw = (u64)(blockIdx.x & ((1u << wshift) - 1u)) * ppw + (blockIdx.x >> wshift);
+    // (window index from block bits [wbit, wbit + wshift); ppw is a multiple of 2^wbit)
+    const u32 bx = blockIdx.x;
+    const u64 pw = (u64)((bx >> wbit) & ((1u << wshift) - 1u)) * ppw +
+                   (((bx >> (wbit + wshift)) << wbit) | (bx & ((1u << wbit) - 1u)));
     const bool pvalid = pw < npieces;
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
@@ -436,6 +439,7 @@ int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, 
 int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
 int ws_piece_occ = 0;     // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
+int ws_piece_wbit = 0;    // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
 int ws_piece_win = 1;     // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
@@ -451,10 +455,11 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
         k = ws_piece_occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
     u32 wshift = (u32)(ws_piece_win < 0 ? 0 : (ws_piece_win > 6 ? 6 : ws_piece_win));
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
-    const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
+    const u32 wbit = wshift ? (u32)(ws_piece_wbit < 0 ? 0 : (ws_piece_wbit > 8 ? 8 : ws_piece_wbit)) : 0u;
+    const u64 ppw = (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
     hipLaunchKernelGGL(k, dim3((u32)(ppw << wshift)), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                        L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
-                       L.desc, L.res, wshift, ppw, (u64)P.npieces);
+                       L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
 }
