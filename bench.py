@@ -635,7 +635,7 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
     ap.add_argument("--fps", type=int, default=None, help="override frames per rx segment (experiments)")
     ap.add_argument("--plen", type=int, default=None, help="override the fixed payload length (experiments)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=1,
                     help="decode: also time K independent batches of the config in flight together, one HIP "
                          "stream each (a reactor with successive rx batches), reported as the 'inflight' field "
                          "(1 = off)")
