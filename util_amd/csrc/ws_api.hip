@@ -29,6 +29,7 @@ extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_piece_win;
 extern int ws_piece_wbit;
+extern int ws_scan_win;
 extern int ws_enc_win;
 int ws_seg_win = 1;       // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern int ws_reasm_merge;
@@ -84,6 +85,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_win")) ws_piece_win = (int)value;
     else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
     else if (!strcmp(name, "piece_wbit")) ws_piece_wbit = (int)value;
+    else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
     else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;

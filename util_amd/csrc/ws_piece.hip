@@ -125,11 +125,11 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 WebsocketSegResult_t* __restrict__ res,
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
-                                                                u32 gen, u64 pbase, u64 lo, u64 hi) {
+                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32 half) {
     static_assert(G == 8 || G == 16 || G == 32 || G == 64, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
-    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / G;
+    const u32 s = (ws_win2(blockIdx.x, half) * PSCAN_T + threadIdx.x) / G;  // half > 0: two windows
     bool active = s < nseg;
     const u32 sc = active ? s : nseg - 1;                                    // inactive groups: harmless loads
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
@@ -379,6 +379,8 @@ extern int ws_dbg_flags;
 int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
 
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
+int ws_scan_win = 0;      // "scan_win": K1 takes its segment groups in two windows (ws_win2)
+
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
@@ -396,15 +398,16 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     if (ws_piece_scan >= 1 && ws_piece_scan <= 4) {
         const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : (ws_piece_scan == 3 ? 16 : 8));
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
+        const u32 half = ws_scan_win && blocks >= 512 ? (blocks + 1) / 2 : 0;
         auto k = G == 64 ? ws_piece_scan_kernel<64>
                          : (G == 32 ? ws_piece_scan_kernel<32> : (G == 16 ? ws_piece_scan_kernel<16> : ws_piece_scan_kernel<8>));
         // A/B tooling only (results wrong): "debug" bit 1 skips descriptor stores, bit 2 items + pointers
         if (G == 16 && (ws_dbg_flags & 6))
             k = (ws_dbg_flags & 6) == 2 ? ws_piece_scan_kernel<16, 2>
                                         : ((ws_dbg_flags & 6) == 4 ? ws_piece_scan_kernel<16, 4> : ws_piece_scan_kernel<16, 6>);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                           L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr, P.disorder, gen,
-                           P.pbase, lo, hi);
+        hipLaunchKernelGGL(k, dim3(half ? 2 * half : blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
+                           L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
+                           P.disorder, gen, P.pbase, lo, hi, half);
     } else {
         hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items,
