@@ -30,6 +30,7 @@ extern int ws_piece_occ;
 extern int ws_piece_win;
 extern int ws_piece_wbit;
 extern int ws_scan_win;
+extern int ws_piece_wn;
 extern int ws_enc_win;
 int ws_seg_win = 1;       // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern int ws_reasm_merge;
@@ -86,7 +87,14 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
     else if (!strcmp(name, "piece_wbit")) ws_piece_wbit = (int)value;
     else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
+    else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;
     else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
+    else if (!strcmp(name, "k2_timing")) {
+        extern int ws_k2_timing;
+        extern void ws_k2_timing_reset();
+        ws_k2_timing = (int)value;
+        ws_k2_timing_reset();
+    }
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
     else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
@@ -96,6 +104,13 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value) {
     if (!value) return -1;
+    unsigned long long ns = 0, calls = 0;
+    if (!strcmp(name, "k2_ns") || !strcmp(name, "k2_calls")) {
+        extern int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
+        if (ws_k2_stat(&ns, &calls)) return -1;
+        *value = name[3] == 'n' ? ns : calls;
+        return 0;
+    }
     if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks;
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks;
     else return -1;

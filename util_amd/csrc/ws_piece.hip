@@ -23,6 +23,9 @@
 //   touched by exactly one block, so no byte is stored twice.
 // Fallback: if the segments are not in ascending buffer order, K2 stores nothing and a
 //   gated walker (ws_walker.hip) decodes the batch.
+#include <mutex>
+#include <vector>
+
 #include "ws_walk.h"
 
 #define PIECE_T 256
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
                                                                   WebsocketSegResult_t* __restrict__ res,
-                                                                  u32 wshift, u32 wbit, u64 ppw, u64 npieces) {
+                                                                  u32 wshift, u32 wbit, u64 ppw, u64 npieces, u32 wn) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
@@ -240,8 +243,10 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     // clamped piece and store nothing
     // (window index from block bits [wbit, wbit + wshift); ppw is a multiple of 2^wbit)
     const u32 bx = blockIdx.x;
-    const u64 pw = (u64)((bx >> wbit) & ((1u << wshift) - 1u)) * ppw +
-                   (((bx >> (wbit + wshift)) << wbit) | (bx & ((1u << wbit) - 1u)));
+    // (wn > 0: wn windows of any count, block b -> (b mod wn) * ppw + b / wn)
+    const u64 pw = wn ? (u64)(bx % wn) * ppw + bx / wn
+                      : (u64)((bx >> wbit) & ((1u << wshift) - 1u)) * ppw +
+                            (((bx >> (wbit + wshift)) << wbit) | (bx & ((1u << wbit) - 1u)));
     const bool pvalid = pw < npieces;
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
@@ -442,12 +447,58 @@ int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, 
 int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
 int ws_piece_occ = 0;     // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
+int ws_piece_wn = 0;      // "piece_wn": >= 2 windows of any count (overrides piece_win/piece_wbit)
 int ws_piece_wbit = 0;    // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
 int ws_piece_win = 1;     // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
+// "k2_timing" (measurement only, bench.py): a pair of HIP events is recorded around every
+// K2 launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
+// recorded K2 durations, "k2_calls" counts them; setting the option clears the record.
+int ws_k2_timing = 0;
+static std::vector<hipEvent_t> g_k2ev;    // start, end, start, end, ...
+static size_t g_k2n = 0;
+static std::mutex g_k2mu;
+
+void ws_k2_timing_reset() {
+    std::lock_guard<std::mutex> lk(g_k2mu);
+    g_k2n = 0;
+}
+
+int ws_k2_stat(unsigned long long* ns, unsigned long long* calls) {
+    std::lock_guard<std::mutex> lk(g_k2mu);
+    double total = 0.0;
+    for (size_t i = 0; i < g_k2n; ++i) {
+        float ms = 0.f;
+        hipError_t e = hipEventSynchronize(g_k2ev[2 * i + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, g_k2ev[2 * i], g_k2ev[2 * i + 1]);
+        if (e != hipSuccess) return ws_set_err("k2 timing events", e);
+        total += ms;
+    }
+    *ns = (unsigned long long)(total * 1e6);
+    *calls = g_k2n;
+    return 0;
+}
+
+static int k2_mark(hipStream_t st, bool end, size_t* slot) {
+    std::lock_guard<std::mutex> lk(g_k2mu);
+    if (!end) *slot = g_k2n++;
+    const size_t i = 2 * *slot + (end ? 1 : 0);
+    hipError_t e;
+    while (g_k2ev.size() <= i) {
+        hipEvent_t ev;
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return ws_set_err("hipEventCreate", e);
+        g_k2ev.push_back(ev);
+    }
+    if ((e = hipEventRecord(g_k2ev[i], st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+    return 0;
+}
+
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
     if (!P.npieces) return 0;
+    size_t tslot = 0;
+    int rc;
+    if (ws_k2_timing && (rc = k2_mark(L.stream, false, &tslot))) return rc;
     auto k = nt == 1 ? (ws_piece_whole == 2 ? ws_piece_unmask_kernel<1, 2, 1>
                                             : (ws_piece_whole == 1 ? ws_piece_unmask_kernel<1, 1, 1>
                                                                    : ws_piece_unmask_kernel<1, 0, 1>))
@@ -459,12 +510,16 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
     u32 wshift = (u32)(ws_piece_win < 0 ? 0 : (ws_piece_win > 6 ? 6 : ws_piece_win));
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
     const u32 wbit = wshift ? (u32)(ws_piece_wbit < 0 ? 0 : (ws_piece_wbit > 8 ? 8 : ws_piece_wbit)) : 0u;
-    const u64 ppw = (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
-    hipLaunchKernelGGL(k, dim3((u32)(ppw << wshift)), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
+    const u32 wn = ws_piece_wn >= 2 && (P.npieces / (u64)ws_piece_wn) >= 256 ? (u32)ws_piece_wn : 0u;
+    const u64 ppw = wn ? (P.npieces + wn - 1) / wn
+                       : (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
+    const u64 grid = wn ? ppw * wn : ppw << wshift;
+    hipLaunchKernelGGL(k, dim3((u32)grid), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                        L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
-                       L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces);
+                       L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces, wn);
     const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : ws_set_err("ws_piece_unmask_kernel launch", e);
+    if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
+    return ws_k2_timing ? k2_mark(L.stream, true, &tslot) : 0;
 }
 
 // K1 + K2; K2 also holds the fallback for unordered batches. *fallback_needed: no K2
