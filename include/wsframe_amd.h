@@ -180,14 +180,19 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * 1 fused, 2 three-kernel), "reasm_cfg", "encode_side", "host_chunk_mb", "dyn"
  * (1 dynamic segment dequeue / 0 static), "unroll" (2|4|8 x 16-B chunks per lane per
  * batch), "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
- * "blocks_per_cu" (0 = resident limit). Returns 0, or -1 for an unknown name. Not
+ * "blocks_per_cu" (0 = resident limit), "piece_win" (log2 of the windows the unmask
+ * kernel streams side by side, default 1), "piece_wn" / "piece_wbit" (other window
+ * maps), "seg_win" / "scan_win" / "enc_win" (two windows for the segment kernels / the
+ * walk / encode), "k2_timing" (see websocketframeGpuGetStat). Returns 0, or -1 for an unknown name. Not
  * thread-safe against concurrent calls. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
 /* Counters of the calling process's most recent call (diagnostics): "stream_rw_chunks"
  * (chunks of a long stream written from the chunk-parallel walk's records),
- * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront). Returns 0, or -1
- * for an unknown name. */
+ * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront); with the option
+ * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece
+ * path's unmask launches since the option was set, from HIP events around each launch;
+ * reading them waits for those launches). Returns 0, or -1 for an unknown name. */
 WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value);
 
 /* ---- Part 2b: fused decode + fragmented-message reassembly -- */

@@ -29,6 +29,9 @@ extern int ws_piece_whole;
 extern int ws_piece_occ;
 extern int ws_piece_win;
 extern int ws_piece_wbit;
+extern int ws_k2_timing;
+void ws_k2_timing_reset();
+int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern int ws_scan_win;
 extern int ws_piece_wn;
 extern int ws_enc_win;
@@ -90,8 +93,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;
     else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
     else if (!strcmp(name, "k2_timing")) {
-        extern int ws_k2_timing;
-        extern void ws_k2_timing_reset();
         ws_k2_timing = (int)value;
         ws_k2_timing_reset();
     }
@@ -106,7 +107,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     if (!value) return -1;
     unsigned long long ns = 0, calls = 0;
     if (!strcmp(name, "k2_ns") || !strcmp(name, "k2_calls")) {
-        extern int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
         if (ws_k2_stat(&ns, &calls)) return -1;
         *value = name[3] == 'n' ? ns : calls;
         return 0;
