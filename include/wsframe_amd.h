@@ -40,6 +40,24 @@ enum {
 
 #define WEBSOCKET_MAX_ENCODE_HEADLENGTH 10
 
+/* websocketframe.h:21-36: the client handshake request templates (path, key[, protocol]) */
+#define WEBSOCKET_SIMPLE_HTTP_HANDSHAKE_REQUEST_FMT \
+    "GET %s HTTP/1.1\r\n"                          \
+    "Upgrade: websocket\r\n"                       \
+    "Connection: Upgrade\r\n"                      \
+    "Sec-WebSocket-Version: 13\r\n"                \
+    "Sec-WebSocket-Key: %s\r\n"                    \
+    "\r\n"
+
+#define WEBSOCKET_SIMPLE_HTTP_HANDSHAKE_REQUEST_WITH_PROTOCOL_FMT \
+    "GET %s HTTP/1.1\r\n"                                        \
+    "Upgrade: websocket\r\n"                                     \
+    "Connection: Upgrade\r\n"                                    \
+    "Sec-WebSocket-Version: 13\r\n"                              \
+    "Sec-WebSocket-Key: %s\r\n"                                  \
+    "Sec-WebSocket-Protocol: %s\r\n"                             \
+    "\r\n"
+
 /* websocketframe.c:16-32 */
 WSFRAME_AMD_EXPORT char* websocketframeComputeSecAccept(const char* sec_key, unsigned int sec_keylen,
                                                         char sec_accept[60]);
@@ -93,9 +111,15 @@ enum {
     WEBSOCKET_SEG_ERR_LEN_WRAP = -2,   /* masked frame whose u64 length sum wraps (websocketframe.c:149):
                                           the reference would unmask past the buffer (undefined behaviour);
                                           fenced off here, nothing is written for that frame */
-    WEBSOCKET_SEG_ERR_OUT_SPACE = -3   /* reassembly only: the bodies outgrow the segment's output region
+    WEBSOCKET_SEG_ERR_OUT_SPACE = -3,  /* reassembly only: the bodies outgrow the segment's output region
                                           (possible only through the (int) return truncation of frames
                                           >= 2 GiB, websocketframe.c:164) */
+    WEBSOCKET_SEG_ERR_CACHE_OVERFLOW = -4 /* reassembly only: caching this frame's body would take the
+                                          connection's cached bytes past readcache_max_size
+                                          (check_cache_overflow, net_channel_ex.c:45-53,132-135); the
+                                          reactor detaches the channel (NET_REACTOR_CACHE_READ_OVERFLOW_ERR).
+                                          Its descriptor is written and counted in n_frames, it is not
+                                          consumed, and no body or message is emitted for it */
 };
 
 /* Per-segment result. 16 bytes. */
@@ -226,6 +250,23 @@ WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(const unsigned char* 
                                                            WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
                                                            unsigned char* d_open, void* hip_stream);
 
+/* The same with the stream hook's fragment-cache limit (NetChannel_t.readcache_max_size,
+ * net_reactor.h:100; 0 = unlimited, as websocketframeBatchReassembleDevice): a frame that is
+ * cached (one arriving while a message is pending, or a non-FIN one) and whose body would
+ * take the pending message's cached bytes past the limit stops its segment with
+ * WEBSOCKET_SEG_ERR_CACHE_OVERFLOW (net_channel_ex.c:129-135). d_cached (optional, one u32
+ * per segment, in/out): the pending message's cached bytes, counted as the reference's u32
+ * StreamTransportCtx_t.cache_recv_bytes (transport_ctx.c:179-201); 0 whenever d_open is 0. */
+WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(const unsigned char* d_buf, unsigned long long buflen,
+                                                             const unsigned long long* d_seg_off,
+                                                             const unsigned long long* d_seg_len, unsigned int nseg,
+                                                             unsigned int max_frames, WebsocketFrameDesc_t* d_desc,
+                                                             WebsocketSegResult_t* d_res, unsigned char* d_out,
+                                                             const unsigned long long* d_out_off,
+                                                             WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
+                                                             unsigned char* d_open, unsigned int readcache_max_size,
+                                                             unsigned int* d_cached, void* hip_stream);
+
 /* ---- Part 2c: batch encode + client masking -------------- */
 
 /* One frame to emit. The header is exactly websocketframeEncode's
@@ -251,35 +292,6 @@ WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_sr
                                                        const WebsocketEncodeDesc_t* d_frames, unsigned int nframes,
                                                        unsigned char* d_dst, unsigned long long dst_capacity,
                                                        unsigned long long* d_wire_off, void* hip_stream);
-
-/* ---- Part 3: synthetic batches (bench / test input only, not the decode path) - */
-
-/* Fill d_buf with nframes masked frames generated by util_amd/csrc/ws_synth.h.
- * d_frame_off[f] = wire offset of frame f (device, exclusive prefix sum of
- * ws_synth_wirelen). plen_kind/b0_kind: WS_PLEN_* / WS_B0_* of ws_synth.h. */
-WSFRAME_AMD_EXPORT int websocketframeSynthDevice(unsigned char* d_buf, const unsigned long long* d_frame_off,
-                                                 unsigned long long nframes, int plen_kind,
-                                                 unsigned long long fixed_len, int b0_kind,
-                                                 unsigned long long seed, void* hip_stream);
-
-/* Count bytes of decoded payloads that differ from the generator's plaintext
- * (size-independent full-batch check). Adds into *d_mismatch (device u64). */
-WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned char* d_buf,
-                                                       const unsigned long long* d_frame_off,
-                                                       unsigned long long nframes, int plen_kind,
-                                                       unsigned long long fixed_len, unsigned long long seed,
-                                                       int expect_plain, unsigned long long* d_mismatch,
-                                                       void* hip_stream);
-
-/* ---- Part 4: diagnostics (not the decode path) --------------------------------- */
-
-/* Streaming-bandwidth ceilings of this device for the decode's access pattern:
- * flat grid-stride 16-B-per-lane kernels over nbytes (multiple of 16).
- * mode 0: in-place XOR of d_a; 1: copy d_a -> d_b; 2: read-only d_a (d_b: 8-B sink);
- * 3: in-place XOR software-pipelined (next loads before current stores); 4: in-place XOR one-shot blocks.
- * nt: nontemporal loads/stores; blocks: grid size (0 = 2048). Async on hip_stream. */
-WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_b, unsigned long long nbytes, int mode, int nt,
-                                                  int blocks, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -2,20 +2,27 @@
  * drop_in.c — a C caller written against the reference's websocketframe API
  * (inc/crt/protocol/websocketframe.h:42-49), the way reactor glue uses it, linked
  * against libwsframe_amd.so instead of websocketframe.c. Host symbols only (no GPU).
- * Built and run by tests/test_abi.py::test_c_program_links_and_runs.
+ * Built and run by tests/test_abi.py: against include/wsframe_amd.h, and (dev container)
+ * against the REFERENCE's own header inc/crt/protocol/websocketframe.h
+ * (-DWS_API_HEADER='"crt/protocol/websocketframe.h"' -I /root/reference/inc): a source
+ * file written for the reference compiles unchanged and links to libwsframe_amd.so.
  *
  * 1. encode a header with websocketframeEncode, mask the payload like a client, then
  *    decode it with the reference's per-frame loop (net_reactor.c:515-526) and check
  *    the out-params and the unmasked bytes;
  * 2. RFC 6455 §1.3 handshake sample through websocketframeComputeSecAccept and the
- *    response encoders.
+ *    response encoders; a request built from WEBSOCKET_SIMPLE_HTTP_HANDSHAKE_REQUEST_FMT
+ *    (websocketframe.h:21-36) parsed back by websocketframeDecodeHandshakeRequest.
  * Prints "drop_in ok" and exits 0 on success.
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include "wsframe_amd.h"
+#ifndef WS_API_HEADER
+#define WS_API_HEADER "wsframe_amd.h"
+#endif
+#include WS_API_HEADER
 
 static int fail(const char* what) {
     fprintf(stderr, "drop_in: %s\n", what);
@@ -72,6 +79,22 @@ int main(void) {
         r2 = websocketframeEncodeHandshakeResponseWithProtocol(acc, (unsigned int)strlen(acc), "chat", 4);
         if (!r2 || !strstr(r2, "Sec-WebSocket-Protocol: chat")) return fail("protocol response");
         websocketframeFreeString(r2);
+    }
+    /* the request templates (websocketframe.h:21-36) round-trip through the request parser */
+    {
+        char req[512];
+        const char *sk = NULL, *sp = NULL;
+        unsigned int skl = 0, spl = 0;
+        snprintf(req, sizeof(req), WEBSOCKET_SIMPLE_HTTP_HANDSHAKE_REQUEST_WITH_PROTOCOL_FMT, "/chat",
+                 "dGhlIHNhbXBsZSBub25jZQ==", "superchat");
+        if (!websocketframeDecodeHandshakeRequest(req, (unsigned int)strlen(req), &sk, &skl, &sp, &spl))
+            return fail("request parse");
+        if (skl != 24 || strncmp(sk, "dGhlIHNhbXBsZSBub25jZQ==", 24)) return fail("request key");
+        if (spl != 9 || strncmp(sp, "superchat", 9)) return fail("request protocol");
+        snprintf(req, sizeof(req), WEBSOCKET_SIMPLE_HTTP_HANDSHAKE_REQUEST_FMT, "/", "x3JJHMbDL1EzLkh9GBhXDw==");
+        if (!websocketframeDecodeHandshakeRequest(req, (unsigned int)strlen(req), &sk, &skl, &sp, &spl))
+            return fail("request parse 2");
+        if (skl != 24 || strncmp(sk, "x3JJHMbDL1EzLkh9GBhXDw==", 24)) return fail("request key 2");
     }
     printf("drop_in ok\n");
     return 0;

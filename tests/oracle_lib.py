@@ -82,21 +82,36 @@ def oracle_encode_frames(src, frames):
     return bytes(out), np.array(offs, dtype=np.uint64)
 
 
-def oracle_reassemble(wire, seg_off, seg_len, max_frames, open_in=None, out_off=None):
-    """Checker for websocketframeBatchReassembleDevice, composed from the decode oracle
+def cache_overflow(already, add, max_limit):
+    """check_cache_overflow (net_channel_ex.c:45-53), u32 operands"""
+    if max_limit == 0:
+        return False
+    if max_limit < add:
+        return True
+    return already > max_limit - add
+
+
+def oracle_reassemble(wire, seg_off, seg_len, max_frames, open_in=None, out_off=None, readcache_max=0,
+                      cached_in=None):
+    """Checker for websocketframeBatchReassembleDevice(Ex), composed from the decode oracle
     (pinned to the reference's golden vectors): the a5 loop runs on a copy of the wire
-    (unmasking in place, as websocketframeDecode does), then the delivery rule of
-    SURVEY §8a row a6 is applied per segment — the bodies of consecutive consumed frames
-    form the pending message, a FIN frame closes it.
+    (unmasking in place, as websocketframeDecode does), then the stream hook's delivery rule
+    (net_channel_ex.c:110-157, pinned to the reference's own reactor by
+    tests/golden/reassemble.json) is applied per segment — the bodies of consecutive consumed
+    frames form the pending message, a FIN frame closes it; a frame that is cached (arriving
+    while a message is pending, or non-FIN) and would take the cached bytes (u32, as
+    cache_recv_bytes) past readcache_max stops the segment: WEBSOCKET_SEG_ERR_CACHE_OVERFLOW,
+    its descriptor counted, not consumed.
     Returns (desc, res, msgs[s] = [(out_off, len, first, n, complete, continued)],
-    regions[s] = (out_off, expected body bytes), open_out)."""
+    regions[s] = (out_off, expected body bytes), open_out, cached_out)."""
     buf = np.asarray(wire, dtype=np.uint8).copy()
     desc, res = oracle_segments(buf, seg_off, seg_len, max_frames)
     res = res.copy()
-    msgs, regions, open_out = [], [], []
+    msgs, regions, open_out, cached_out = [], [], [], []
     for s in range(len(seg_off)):
         ob = int(out_off[s]) if out_off is not None else int(seg_off[s])
         opened = int(open_in[s]) if open_in is not None else 0
+        cached = int(cached_in[s]) & 0xFFFFFFFF if (cached_in is not None and opened) else 0
         cont, first, q, q0 = opened, 0, 0, 0
         bodies, ms = [], []
         for k in range(int(res[s]["n_frames"])):
@@ -107,16 +122,42 @@ def oracle_reassemble(wire, seg_off, seg_len, max_frames, open_in=None, out_off=
             if n > int(seg_len[s]) - q:
                 res[s]["status"] = -3
                 break
+            fin = int(d["is_fin"])
+            cache_it = bool(opened) or not fin                          # net_channel_ex.c:129
+            if cache_it and cache_overflow(cached, n & 0xFFFFFFFF, readcache_max):
+                res[s]["status"] = -4
+                res[s]["consumed"] = int(d["frame_off"]) - int(seg_off[s])
+                res[s]["n_frames"] = k + 1
+                break
             a = int(d["data_off"])
             bodies.append(buf[a:a + n] if n else buf[:0])
             q += n
+            if cache_it:
+                cached = (cached + (n & 0xFFFFFFFF)) & 0xFFFFFFFF
             opened = 1
-            if int(d["is_fin"]):
+            if fin:
                 ms.append((ob + q0, q - q0, first, k + 1 - first, 1, cont))
-                first, q0, cont, opened = k + 1, q, 0, 0
+                first, q0, cont, opened, cached = k + 1, q, 0, 0, 0
         if opened and len(bodies) > first:
             ms.append((ob + q0, q - q0, first, len(bodies) - first, 0, cont))
         msgs.append(ms)
         regions.append((ob, np.concatenate(bodies) if bodies else np.zeros(0, np.uint8)))
         open_out.append(opened)
-    return desc, res, msgs, regions, np.array(open_out, dtype=np.uint8)
+        cached_out.append(cached if opened else 0)
+    return desc, res, msgs, regions, np.array(open_out, dtype=np.uint8), np.array(cached_out, dtype=np.uint32)
+
+
+def reactor_view(msgs, regions, res, open_out, cached_out, s=0):
+    """What the reference reactor reports for segment s (one connection's stream), from a
+    reassembly result: (complete message lengths, their bodies back to back, bytes consumed,
+    frames consumed, detach error, pending, cached) — the fields of tests/golden/reassemble.json."""
+    ob, body = regions[s]
+    lens, parts = [], []
+    for (o, n, _first, _nf, complete, _cont) in msgs[s]:
+        if complete:
+            lens.append(int(n))
+            parts.append(body[int(o) - ob:int(o) - ob + int(n)])
+    st = int(res[s]["status"])
+    nf = int(res[s]["n_frames"]) - (1 if st in (-1, -4) else 0)
+    return (lens, np.concatenate(parts) if parts else np.zeros(0, np.uint8), int(res[s]["consumed"]), nf,
+            7 if st == -4 else 0, int(open_out[s]), int(cached_out[s]))

@@ -8,6 +8,7 @@ import re
 import subprocess
 
 import numpy as np
+import pytest
 
 import util_amd
 from util_amd import _lib
@@ -16,22 +17,37 @@ from util_amd import wsframe as W
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_symbols():
-    src = open(os.path.join(REPO, "include", "wsframe_amd.h")).read()
-    return sorted(set(re.findall(r"WSFRAME_AMD_EXPORT[^;]*?\b(websocketframe\w+)\s*\(", src, re.S)))
+REF_INC = "/root/reference/inc"
 
 
-def test_exports_every_declared_symbol():
-    util_amd.load_lib()
+def header_symbols(*names):
+    out = set()
+    for n in names or ("wsframe_amd.h", "wsframe_amd_channel.h"):
+        src = open(os.path.join(REPO, "include", n)).read()
+        out |= set(re.findall(r"WSFRAME_AMD_EXPORT[^;]*?\b(websocketframe\w+)\s*\(", src, re.S))
+    return sorted(out)
+
+
+def dynamic_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_exports_exactly_the_declared_symbols():
+    """libwsframe_amd.so's dynamic symbol table is its C ABI and nothing else: the reference's
+    eight symbols + the batch / glue API of include/wsframe_amd.h + wsframe_amd_channel.h (no
+    kernel stubs, no bench or calibration entry points, no C++ symbols)"""
+    lib = util_amd.load_lib()
     declared = header_symbols()
     assert len(declared) == 19
     assert sorted(_lib.EXPORTS) == declared
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r"\bT (websocketframe\w+)", out))
-    assert set(declared) <= exported, set(declared) - exported
-    lib = util_amd.load_lib()
+    assert dynamic_symbols(_lib.LIB_PATH) == set(declared)
     for s in declared:
         assert getattr(lib, s) is not None
+    bench = header_symbols("wsframe_amd_bench.h")
+    assert sorted(_lib.BENCH_EXPORTS) == bench
+    assert dynamic_symbols(_lib.BENCH_LIB_PATH) == set(bench)
+    _lib.load_bench_lib()
 
 
 def test_reference_signature_set():
@@ -129,15 +145,39 @@ def test_host_decode_word_xor_matches_bytewise():
             assert bytes(buf[align + hl + 4:]) == pay.tobytes()
 
 
+def _build_run(tmp_path, src, name, extra, expect):
+    util_amd.load_lib()
+    exe = str(tmp_path / name)
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror"] + extra +
+                   ["-I", os.path.join(REPO, "include"), os.path.join(REPO, "tests", "c", src), "-L", libdir,
+                    "-lwsframe_amd", "-Wl,-rpath," + libdir, "-o", exe], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == expect
+
+
 def test_c_program_links_and_runs(tmp_path):
     """a C caller of the reference API (tests/c/drop_in.c), compiled against
     include/wsframe_amd.h and linked to libwsframe_amd.so in place of websocketframe.c"""
-    util_amd.load_lib()
-    exe = str(tmp_path / "drop_in")
-    libdir = os.path.dirname(_lib.LIB_PATH)
-    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
-                    os.path.join(REPO, "tests", "c", "drop_in.c"), "-L", libdir, "-lwsframe_amd",
-                    "-Wl,-rpath," + libdir, "-o", exe], check=True)
-    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
-    assert out.returncode == 0, out.stderr
-    assert out.stdout.strip() == "drop_in ok"
+    _build_run(tmp_path, "drop_in.c", "drop_in", [], "drop_in ok")
+
+
+def test_c_program_reference_header(tmp_path):
+    """the same caller compiled against the REFERENCE's own header
+    (inc/crt/protocol/websocketframe.h: enum, WEBSOCKET_MAX_ENCODE_HEADLENGTH, the two handshake
+    request templates, the eight prototypes) links to libwsframe_amd.so unchanged"""
+    if not os.path.isdir(REF_INC):
+        pytest.skip("reference headers not present (GPU box)")
+    _build_run(tmp_path, "drop_in.c", "drop_in_ref",
+               ["-I", REF_INC, '-DWS_API_HEADER="crt/protocol/websocketframe.h"', "-Wno-unused-function"], "drop_in ok")
+
+
+def test_channel_glue_layout(tmp_path):
+    """include/wsframe_amd_channel.h against the reference's net_channel_ex.h: identical
+    NetChannelInbufDecodeResult_t layout, websocketframeOnDecode assignable to
+    NetChannelExProc_t.on_decode, NETPACKET_FRAGMENT value; the glue runs"""
+    if not os.path.isdir(REF_INC):
+        pytest.skip("reference headers not present (GPU box)")
+    _build_run(tmp_path, "channel_layout.c", "channel_layout", ["-I", REF_INC, "-D_GNU_SOURCE", "-Wno-unused-function"],
+               "channel_layout ok")

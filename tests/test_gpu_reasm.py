@@ -1,8 +1,10 @@
-"""GPU parity of websocketframeBatchReassembleDevice (fused decode + message reassembly,
-SURVEY §8a row a6) against the oracle composition (tests/oracle_lib.py:
-oracle_reassemble = the pinned decode oracle + the FIN delivery rule), bit-exact:
-descriptors, segment results, message descriptors, gathered bodies, open state; the
-wire must come back untouched."""
+"""GPU parity of websocketframeBatchReassembleDevice(Ex) (fused decode + message reassembly,
+SURVEY §8a row a6) against the reference's own rx stack (tests/golden/reassemble.json: the
+reactor + stream hook + fragment cache compiled from the reference, oracle/reactor_harness.c)
+and against the oracle composition (tests/oracle_lib.py: oracle_reassemble = the pinned
+decode oracle + the delivery rule + the cache limit, itself pinned to that fixture),
+bit-exact: descriptors, segment results, message descriptors, gathered bodies, open state,
+cached bytes; the wire must come back untouched."""
 import numpy as np
 import pytest
 
@@ -32,7 +34,8 @@ def reasm_path(request):
     W.set_option("reasm_path", 0)
 
 
-def gpu_reassemble(dev, wire, so, sl, max_frames, open_in=None, out_off=None, out_size=None):
+def gpu_reassemble(dev, wire, so, sl, max_frames, open_in=None, out_off=None, out_size=None, readcache_max=0,
+                   cached_in=None):
     n = len(wire)
     d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
     if n:
@@ -45,18 +48,21 @@ def gpu_reassemble(dev, wire, so, sl, max_frames, open_in=None, out_off=None, ou
     res = torch.zeros(max(1, nseg) * 16, dtype=torch.uint8, device=dev)
     nmsg = torch.zeros(max(1, nseg), dtype=torch.int32, device=dev)
     op = None if open_in is None else torch.tensor(np.asarray(open_in, dtype=np.uint8), device=dev)
+    ca = None if cached_in is None else torch.tensor(np.asarray(cached_in, dtype=np.uint32).view(np.int32), device=dev)
     W.batch_reassemble_device(d, T(so), T(sl), max_frames, desc, res, out, msg, nmsg,
-                              out_off=None if out_off is None else T(out_off), open_state=op)
+                              out_off=None if out_off is None else T(out_off), open_state=op,
+                              readcache_max=readcache_max, cached=ca)
     torch.cuda.synchronize()
     assert np.array_equal(d[:n].cpu().numpy(), wire), "wire buffer modified"
     return (out.cpu().numpy(), desc.cpu().numpy().view(W.DESC_DTYPE), res.cpu().numpy().view(W.SEGRES_DTYPE)[:nseg],
             msg.cpu().numpy().view(W.MSG_DTYPE), nmsg.cpu().numpy()[:nseg],
-            None if op is None else op.cpu().numpy())
+            None if op is None else op.cpu().numpy(), None if ca is None else ca.cpu().numpy().view(np.uint32))
 
 
-def check(dev, wire, so, sl, mf, open_in=None, out_off=None, out_size=None, tag=""):
-    out, gd, gr, gm, gn, gop = gpu_reassemble(dev, wire, so, sl, mf, open_in, out_off, out_size)
-    od, orr, oms, oreg, oop = oracle_reassemble(wire, so, sl, mf, open_in, out_off)
+def check(dev, wire, so, sl, mf, open_in=None, out_off=None, out_size=None, tag="", readcache_max=0, cached_in=None):
+    out, gd, gr, gm, gn, gop, gca = gpu_reassemble(dev, wire, so, sl, mf, open_in, out_off, out_size, readcache_max,
+                                                   cached_in)
+    od, orr, oms, oreg, oop, oca = oracle_reassemble(wire, so, sl, mf, open_in, out_off, readcache_max, cached_in)
     assert np.array_equal(gr, orr), tag
     assert np.array_equal(used_descs(gd, gr, mf), used_descs(od, orr, mf)), tag
     for s in range(len(so)):
@@ -68,6 +74,8 @@ def check(dev, wire, so, sl, mf, open_in=None, out_off=None, out_size=None, tag=
         assert np.array_equal(out[ob:ob + len(body)], body), (tag, s)
     if open_in is not None:
         assert np.array_equal(gop, oop), tag
+    if cached_in is not None:
+        assert np.array_equal(gca, oca), tag
     return out, oms, oop
 
 
@@ -78,7 +86,7 @@ def test_reassemble_random_vs_oracle(dev, seed, mf):
     out, _, _ = check(dev, wire, so, sl, mf, tag="seed %d" % seed)
     # bytes between the gathered bodies of different segments stay untouched
     covered = np.zeros(len(wire) + 64, bool)
-    _, _, _, oreg, _ = oracle_reassemble(wire, so, sl, mf)
+    _, _, _, oreg, _, _ = oracle_reassemble(wire, so, sl, mf)
     for ob, body in oreg:
         covered[ob:ob + len(body)] = True
     assert (out[~covered] == 0xEE).all()
@@ -191,7 +199,7 @@ def test_reassemble_length_quirks(dev):
             parts.insert(int(rng.integers(0, len(parts) + 1)), mwrap)
         segs.append(parts)
     wire, so, sl = _segments(segs, rng)
-    _, orr, _, _, _ = oracle_reassemble(wire, so, sl, 16)
+    _, orr, _, _, _, _ = oracle_reassemble(wire, so, sl, 16)
     assert (orr["status"] == -3).any() and (orr["status"] == -2).any()
     check(dev, wire, so, sl, 16, tag="quirks")
 
@@ -209,3 +217,69 @@ def test_reassemble_int_truncation_real_size(dev, total):
     wire[:14] = np.frombuffer(bytes([0x02, 0x80 | 127]) + plen.to_bytes(8, "big") + bytes([1, 2, 3, 4]), dtype=np.uint8)
     _, oms, _ = check(dev, wire, [0], [n], 4, out_size=1 << 20, tag="int truncation")
     assert oms == [[]]
+
+
+# ------------------------------------------------------------------ the reference's own deliveries
+
+def _gpu_reactor_view(dev, wire, max_frames, limit):
+    """the stream decoded on the GPU batch after batch (each batch = the bytes from the previous
+    batch's `consumed` on, at most max_frames frames), d_open / d_cached carried across batches:
+    the reference reactor's view (complete messages, consumed, frames, detach error, pending,
+    cached) of the whole stream"""
+    pos, frames, lens, bodies = 0, 0, [], []
+    op, ca = [0], [0]
+    carry = np.zeros(0, np.uint8)
+    while True:
+        seg = wire[pos:]
+        out, gd, gr, gm, gn, op, ca = gpu_reassemble(dev, seg, [0], [len(seg)], max_frames, open_in=op,
+                                                     readcache_max=limit, cached_in=ca)
+        for i in range(int(gn[0])):
+            m = gm[i]
+            part = out[int(m["out_off"]):int(m["out_off"]) + int(m["len"])]
+            whole = np.concatenate([carry, part]) if int(m["continued"]) else part
+            if int(m["complete"]):
+                lens.append(len(whole))
+                bodies.append(whole)
+                carry = np.zeros(0, np.uint8)
+            else:
+                carry = whole
+        st = int(gr[0]["status"])
+        pos += int(gr[0]["consumed"])
+        frames += int(gr[0]["n_frames"]) - (1 if st == -4 else 0)
+        if st != 1:
+            return (lens, np.concatenate(bodies) if bodies else np.zeros(0, np.uint8), pos, frames,
+                    7 if st == -4 else 0, int(op[0]), int(ca[0]))
+
+
+@pytest.mark.parametrize("mf", [16, 64, 0], ids=["mf16", "mf64", "whole"])
+def test_reassemble_reference_reactor_fixture(dev, golden, reasm_path, mf):
+    """every stream of tests/golden/reassemble.json (cfg5 shape, mixed messages with pings inside
+    fragmented ones, open at the end, incomplete tail, fragment-cache overflow at the limit and
+    past it, FIN frames that skip the check, empty fragments): the GPU delivers exactly what the
+    reference's own reactor delivered — message lengths, body bytes (SHA-256), bytes and frames
+    consumed, the detach, the cache state at the end. mf 0 = the whole stream as one segment
+    (three-kernel path only: the fused kernel holds <= 64 frames per segment)."""
+    import reasm_cases as R
+    if mf == 0 and reasm_path == 1:
+        pytest.skip("fused path: max_frames <= 64")
+    for c in golden("reassemble.json"):
+        wire, limit = R.build(c["name"])
+        assert R.sha256(wire) == c["wire_sha256"]
+        lens, bodies, consumed, frames, det, pend, cached = _gpu_reactor_view(dev, wire, mf or c["frames"] + 2, limit)
+        assert lens == c["msg_lens"], c["name"]
+        assert R.sha256(bodies) == c["bodies_sha256"], c["name"]
+        assert (consumed, frames, det, pend, cached) == (c["consumed"], c["frames"], c["detach_error"], c["pending"],
+                                                         c["cached"]), c["name"]
+
+
+@pytest.mark.parametrize("limit", [1, 700, 4096, 65536])
+def test_reassemble_cache_limit_random_vs_oracle(dev, limit):
+    """many connections per batch, random fragmented streams, open/cached state carried in,
+    every readcache_max_size regime: bit-exact vs the oracle (pinned to the reference reactor)"""
+    rng = np.random.default_rng(40 + limit)
+    wire, so, sl = random_stream(rng, 1200)
+    open0 = rng.integers(0, 2, len(so)).astype(np.uint8)
+    cached0 = np.where(open0 == 1, rng.integers(0, 2 * limit, len(so)), 0).astype(np.uint32)
+    od, orr, _, _, _, _ = oracle_reassemble(wire, so, sl, 16, open0, None, limit, cached0)
+    assert (orr["status"] == -4).any(), "the limit never triggered: the case tests nothing"
+    check(dev, wire, so, sl, 16, open_in=open0, readcache_max=limit, cached_in=cached0, tag="limit %d" % limit)

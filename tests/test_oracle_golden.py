@@ -170,9 +170,136 @@ def test_oracle_reassemble_delivery_rule():
         return bytes([b0, 0x80 | len(body)]) + key + masked
     wire = frame(0x02, b"alpha") + frame(0x80, b"beta") + frame(0x81, b"gamma") + frame(0x00, b"delta")
     w = np.frombuffer(wire, dtype=np.uint8)
-    desc, res, msgs, regions, op = oracle_reassemble(w, [0], [len(wire)], 8)
+    desc, res, msgs, regions, op, _ = oracle_reassemble(w, [0], [len(wire)], 8)
     assert int(res[0]["n_frames"]) == 4 and int(res[0]["consumed"]) == len(wire)
     assert [m[1:] for m in msgs[0]] == [(9, 0, 2, 1, 0), (5, 2, 1, 1, 0), (5, 3, 1, 0, 0)]
     assert bytes(regions[0][1]) == b"alphabetagammadelta" and op[0] == 1
-    _, _, msgs2, _, op2 = oracle_reassemble(w, [0], [len(wire)], 8, open_in=[1])
+    _, _, msgs2, _, op2, _ = oracle_reassemble(w, [0], [len(wire)], 8, open_in=[1])
     assert msgs2[0][0][5] == 1 and msgs2[0][1][5] == 0
+
+
+# ------------------------------------------------------------------ reassembly, pinned to the
+# reference's own rx stack (tests/golden/reassemble.json, made by tests/golden/make_reasm_golden.py
+# from NetReactor_handle -> on_read_stream -> fragment cache -> on_recv, oracle/reactor_harness.c)
+
+def _reasm_cases(golden):
+    import reasm_cases as R
+    for c in golden("reassemble.json"):
+        wire, limit = R.build(c["name"])
+        assert R.sha256(wire) == c["wire_sha256"] and len(wire) == c["wire_len"], c["name"]  # stream pinned
+        assert limit == c["readcache_max"]
+        yield c, wire
+
+
+def _fixture_view(c):
+    return (c["msg_lens"], c["bodies_sha256"], c["consumed"], c["frames"], c["detach_error"], c["pending"], c["cached"])
+
+
+def _view_digest(v):
+    import reasm_cases as R
+    lens, bodies, consumed, frames, det, pend, cached = v
+    return (lens, R.sha256(bodies), consumed, frames, det, pend, cached)
+
+
+def test_reassemble_fixture_vs_oracle(golden):
+    """the reassembly checker (oracle_reassemble: decode oracle + delivery rule + cache limit) on
+    each whole stream as one rx segment reproduces the reference reactor's deliveries exactly"""
+    from oracle_lib import oracle_reassemble, reactor_view
+    n = 0
+    for c, wire in _reasm_cases(golden):
+        mf = c["frames"] + 2
+        _, res, msgs, regions, op, cached = oracle_reassemble(wire, [0], [len(wire)], mf,
+                                                             readcache_max=c["readcache_max"])
+        assert _view_digest(reactor_view(msgs, regions, res, op, cached)) == tuple(_fixture_view(c)), c["name"]
+        n += 1
+    assert n == 10
+
+
+def oracle_reassemble_batches(wire, max_frames, limit):
+    """the stream decoded batch after batch (each batch: the bytes from the previous batch's
+    `consumed` on, max_frames frames at most), open state and cached bytes carried across
+    batches; returns the reference-reactor view of the whole stream"""
+    from oracle_lib import oracle_reassemble
+    pos, frames, lens, bodies = 0, 0, [], []
+    op, cached = [0], [0]
+    carry = np.zeros(0, np.uint8)                     # the pending message's bytes from earlier batches
+    while True:
+        seg = wire[pos:]
+        _, res, msgs, regions, op, cached = oracle_reassemble(seg, [0], [len(seg)], max_frames, open_in=op,
+                                                             out_off=[0], readcache_max=limit, cached_in=cached)
+        ob, body = regions[0]
+        for (o, n, _f, _k, complete, cont) in msgs[0]:
+            part = body[int(o):int(o) + int(n)]
+            whole = np.concatenate([carry, part]) if cont else part
+            if complete:
+                lens.append(len(whole))
+                bodies.append(whole)
+                carry = np.zeros(0, np.uint8)
+            else:
+                carry = whole
+        st = int(res[0]["status"])
+        pos += int(res[0]["consumed"])
+        frames += int(res[0]["n_frames"]) - (1 if st == -4 else 0)
+        if st != 1:                                   # anything but MAX_FRAMES ends the stream
+            return (lens, np.concatenate(bodies) if bodies else np.zeros(0, np.uint8), pos, frames,
+                    7 if st == -4 else 0, int(op[0]), int(cached[0]))
+
+
+@pytest.mark.parametrize("mf", [1, 16, 64])
+def test_reassemble_fixture_batches_vs_oracle(golden, mf):
+    """the same streams cut into batches of at most `mf` frames, state carried across batches
+    (d_open / d_cached): deliveries identical to the reference reactor's"""
+    for c, wire in _reasm_cases(golden):
+        if mf == 1 and len(wire) > 3000000:
+            continue
+        v = oracle_reassemble_batches(wire, mf, c["readcache_max"])
+        assert _view_digest(v) == tuple(_fixture_view(c)), (c["name"], mf)
+
+
+def _reference_reactor():
+    import ref_reactor
+    if not ref_reactor.available():
+        pytest.skip("reference build not present (GPU box): tests/golden/reassemble.json carries the pin")
+    return ref_reactor
+
+
+def test_reference_reactor_fuzz_vs_oracle():
+    """dev container only: random streams with random cache limits through the reference's own
+    reactor vs the reassembly checker"""
+    X = _reference_reactor()
+    import reasm_cases as R
+    from oracle_lib import oracle_reassemble, reactor_view
+    rng = np.random.default_rng(99)
+    for i in range(150):
+        parts = []
+        for _ in range(int(rng.integers(0, 25))):
+            nfr = int(rng.integers(1, 6))
+            sizes = [int(rng.choice([0, 1, 50, 125, 126, 700, 3000, 20000])) for _ in range(nfr)]
+            parts.append(R.message(rng, sizes, masked=rng.random() < 0.8, opcode=int(rng.integers(0, 3))))
+            if rng.random() < 0.2:
+                parts.append(R.frame(rng, int(rng.choice([0x89, 0x8A, 0x00, 0x02])), int(rng.integers(0, 125))))
+        wire = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+        if rng.random() < 0.3 and len(wire):
+            wire = wire[:int(rng.integers(0, len(wire)))]
+        limit = int(rng.choice([0, 0, 100, 1000, 5000, 30000]))
+        r = X.reactor_deliver(wire, int(rng.choice([3, 100, 4096, 1 << 20])), limit)
+        _, res, msgs, regions, op, cached = oracle_reassemble(wire, [0], [len(wire)], r["frames"] + 2,
+                                                             readcache_max=limit)
+        v = reactor_view(msgs, regions, res, op, cached)
+        assert v[0] == r["lens"] and np.array_equal(v[1], r["bodies"]), i
+        assert v[2:] == (r["consumed"], r["frames"], r["detach_error"], r["pending"], r["cached"]), i
+
+
+def test_reference_reactor_with_amd_glue(golden):
+    """the drop-in at the plugin seam: the reference's reactor + stream hook with
+    NetChannelExProc_t.on_decode = libwsframe_amd.so's websocketframeOnDecode (our host decode
+    and glue, include/wsframe_amd_channel.h) delivers exactly what it delivers with the
+    reference's own websocketframeDecode (the fixture)"""
+    X = _reference_reactor()
+    import reasm_cases as R
+    from util_amd import load_lib
+    glue = C.cast(load_lib().websocketframeOnDecode, C.c_void_p).value
+    for c, wire in _reasm_cases(golden):
+        r = X.reactor_deliver(wire, 1500, c["readcache_max"], on_decode=glue)
+        v = (r["lens"], R.sha256(r["bodies"]), r["consumed"], r["frames"], r["detach_error"], r["pending"], r["cached"])
+        assert v == tuple(_fixture_view(c)), c["name"]

@@ -9,7 +9,10 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "libwsframe_amd.so")
+# bench / test support (synthetic batches generated in HBM, calibration): NOT the drop-in
+BENCH_LIB_PATH = os.path.join(HERE, "libwsframe_amd_bench.so")
 _lib = None
+_bench = None
 
 
 class WsDesc(C.Structure):
@@ -22,16 +25,25 @@ class WsSegRes(C.Structure):
     _fields_ = [("consumed", C.c_ulonglong), ("n_frames", C.c_uint), ("status", C.c_int)]
 
 
-# every symbol include/wsframe_amd.h declares
-EXPORTS = [
+# the reference's eight symbols (inc/crt/protocol/websocketframe.h:42-49)
+REFERENCE_EXPORTS = [
     "websocketframeComputeSecAccept", "websocketframeDecodeHandshakeRequest",
     "websocketframeEncodeHandshakeResponse", "websocketframeEncodeHandshakeResponseWithProtocol",
     "websocketframeFreeString", "websocketframeDecode", "websocketframeEncodeHeadLength",
-    "websocketframeEncode", "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
-    "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice", "websocketframeStreamDecodeDevice",
-    "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuGetStat",
-    "websocketframeGpuCalibrate", "websocketframeSynthDevice", "websocketframeSynthVerifyDevice",
+    "websocketframeEncode",
 ]
+# every symbol include/wsframe_amd.h + include/wsframe_amd_channel.h declare: the whole
+# dynamic symbol table of libwsframe_amd.so
+EXPORTS = REFERENCE_EXPORTS + [
+    "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
+    "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice",
+    "websocketframeBatchReassembleDeviceEx", "websocketframeStreamDecodeDevice",
+    "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuGetStat",
+    "websocketframeOnDecode", "websocketframeOnDecodeBatch",
+]
+# include/wsframe_amd_bench.h (libwsframe_amd_bench.so)
+BENCH_EXPORTS = ["websocketframeSynthDevice", "websocketframeSynthVerifyDevice", "websocketframeGpuCalibrate",
+                 "websocketframeBenchLastError"]
 
 
 def build_lib(force=False):
@@ -83,12 +95,11 @@ def load_lib():
     lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
     lib.websocketframeGpuGetStat.restype = i32
     lib.websocketframeGpuGetStat.argtypes = [C.c_char_p, P(C.c_ulonglong)]
-    lib.websocketframeGpuCalibrate.restype = i32
-    lib.websocketframeGpuCalibrate.argtypes = [vp, vp, u64, i32, i32, i32, vp]
-    lib.websocketframeSynthDevice.restype = i32
-    lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
-    lib.websocketframeSynthVerifyDevice.restype = i32
-    lib.websocketframeSynthVerifyDevice.argtypes = [vp, vp, u64, i32, u64, u64, i32, vp, vp]
+    lib.websocketframeBatchReassembleDeviceEx.restype = i32
+    lib.websocketframeBatchReassembleDeviceEx.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, vp, vp, vp, vp, vp, u32, vp,
+                                                          vp]
+    lib.websocketframeOnDecode.restype = None
+    lib.websocketframeOnDecode.argtypes = [vp, vp, C.c_size_t, vp]
     # launch tuning from the environment, e.g. WSFRAME_AMD_OPTIONS="path=0,seg_cfg=10"
     for kv in filter(None, os.environ.get("WSFRAME_AMD_OPTIONS", "").split(",")):
         name, _, value = kv.partition("=")
@@ -98,7 +109,34 @@ def load_lib():
     return lib
 
 
+def load_bench_lib():
+    """libwsframe_amd_bench.so: synthetic batches in HBM + calibration kernels (bench/tests)"""
+    global _bench
+    if _bench is not None:
+        return _bench
+    if not os.path.exists(BENCH_LIB_PATH):
+        raise RuntimeError("libwsframe_amd_bench.so not built: run __graft_entry__.build()")
+    lib = C.CDLL(BENCH_LIB_PATH)
+    vp, u64, i32 = C.c_void_p, C.c_ulonglong, C.c_int
+    lib.websocketframeGpuCalibrate.restype = i32
+    lib.websocketframeGpuCalibrate.argtypes = [vp, vp, u64, i32, i32, i32, vp]
+    lib.websocketframeSynthDevice.restype = i32
+    lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
+    lib.websocketframeSynthVerifyDevice.restype = i32
+    lib.websocketframeSynthVerifyDevice.argtypes = [vp, vp, u64, i32, u64, u64, i32, vp, vp]
+    lib.websocketframeBenchLastError.restype = C.c_char_p
+    lib.websocketframeBenchLastError.argtypes = []
+    _bench = lib
+    return lib
+
+
 def check(rc, what):
     if rc != 0:
         err = load_lib().websocketframeGpuLastError().decode(errors="replace")
+        raise RuntimeError("%s failed (%d): %s" % (what, rc, err))
+
+
+def check_bench(rc, what):
+    if rc != 0:
+        err = load_bench_lib().websocketframeBenchLastError().decode(errors="replace")
         raise RuntimeError("%s failed (%d): %s" % (what, rc, err))

@@ -3,10 +3,13 @@
 // ws_hostpath.hip).
 //
 // Default path 3 = ws_piece.hip (walk kernel + one-shot unmask over 16 KiB pieces;
-// fastest measured). Variants kept for A/B measurement: 1 "walker" =
-// ws_walker.hip (one wave walks and unmasks one segment; also the gated fallback of
-// path 3 for unordered segments), 0 "segblock" = ws_segblock.hip (one workgroup per
-// segment), 2 "split" = ws_split.hip (walk kernel + one block per segment).
+// fastest measured); path 4 = ws_segfuse.hip (one workgroup per segment,
+// auto for many small segments); path 1 "walker" = ws_walker.hip (one wave walks and
+// unmasks one segment; also the gated fallback of path 3 for unordered segments).
+//
+// Options (websocketframeGpuSetOption) are std::atomic: a call reads each knob once
+// (WsTuning snapshot below) and concurrent SetOption calls never race with a launch.
+// Every option value yields bit-identical results; only the speed differs.
 #include <stdio.h>
 #include <string.h>
 
@@ -17,28 +20,27 @@
 #include "ws_common.h"
 
 static __thread char g_last_error[256];
-extern int ws_dbg_flags;
-extern size_t ws_host_chunk_bytes;
-extern int ws_piece_scan;
-extern int ws_reasm_path;
-extern int ws_reasm_cfg;
-extern int ws_segfuse_cfg;
-extern int ws_encode_side;
-extern int ws_encode_fused;
-extern int ws_piece_whole;
-extern int ws_piece_occ;
-extern int ws_piece_win;
-extern int ws_piece_wbit;
-extern int ws_k2_timing;
+extern std::atomic<size_t> ws_host_chunk_bytes;
+extern WsOpt ws_piece_scan;
+extern WsOpt ws_reasm_path;
+extern WsOpt ws_reasm_cfg;
+extern WsOpt ws_segfuse_cfg;
+extern WsOpt ws_encode_side;
+extern WsOpt ws_encode_fused;
+extern WsOpt ws_piece_whole;
+extern WsOpt ws_piece_occ;
+extern WsOpt ws_piece_win;
+extern WsOpt ws_piece_wbit;
+extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
-extern int ws_scan_win;
-extern int ws_piece_wn;
-extern int ws_enc_win;
-int ws_seg_win = 1;       // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
-extern int ws_reasm_merge;
-extern int ws_stream_rw, ws_stream_rw_cmax;
-extern unsigned long long ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
+extern WsOpt ws_scan_win;
+extern WsOpt ws_piece_wn;
+extern WsOpt ws_enc_win;
+WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
+extern WsOpt ws_reasm_merge;
+extern WsOpt ws_stream_rw, ws_stream_rw_cmax;
+extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -56,27 +58,33 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 // launch configuration (tunable for in-process A/B by bench/profiling tools)
 
 struct WsTuning {
-    int path = -1;          // -1 auto (4 for many small segments, else 3), 0: segment blocks (ws_segblock),
-                            // 1: fused walker, 2: split walk + unmask, 3: walk + one-shot 16 KiB pieces
-                            // (ws_piece), 4: one workgroup per segment, walk + unmask fused (ws_segfuse)
-    int seg_cfg = 0;        // segment-block geometry: 0 256x17, 1 512x9, 2 1024x5, 3 256x8, 4 512x4
-    int split_cfg = 0;      // split unmask geometry: 0 512x9, 1 1024x5, 2 256x17, 3 512x4
+    int path = -1;          // -1 auto (4 for many small segments, else 3), 1: walker (one wave per segment),
+                            // 3: walk + one-shot 16 KiB pieces (ws_piece), 4: one workgroup per segment,
+                            // walk + unmask fused (ws_segfuse)
     int nt = 1;             // 0 plain, 1 nontemporal loads+stores, 2 nontemporal stores only
     int dyn = 0;            // walker: 1 dynamic segment dequeue, 0 static grid-stride
     int unroll = 4;         // walker: 16-B chunks per lane per batch
     int blocks_per_cu = 64; // walker: grid cap in blocks per CU (64: one segment per wave)
 };
-static WsTuning g_tune;
+static WsOpt g_path{-1}, g_nt{1}, g_dyn{0}, g_unroll{4}, g_bpc{64};
+static WsTuning tuning() {                        // one consistent read per call
+    WsTuning t;
+    t.path = g_path; t.nt = g_nt; t.dyn = g_dyn; t.unroll = g_unroll; t.blocks_per_cu = g_bpc;
+    return t;
+}
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
-    if (!strcmp(name, "path")) g_tune.path = (int)value;
-    else if (!strcmp(name, "split_cfg")) g_tune.split_cfg = (int)value;
-    else if (!strcmp(name, "seg_cfg")) g_tune.seg_cfg = (int)value;
-    else if (!strcmp(name, "debug")) ws_dbg_flags = (int)value;
-    else if (!strcmp(name, "nt")) g_tune.nt = (int)value;
-    else if (!strcmp(name, "dyn")) g_tune.dyn = (int)value;
-    else if (!strcmp(name, "unroll")) g_tune.unroll = (int)value;
-    else if (!strcmp(name, "blocks_per_cu")) g_tune.blocks_per_cu = (int)value;
+    if (!strcmp(name, "path")) {
+        if (value != -1 && value != 1 && value != 3 && value != 4) return -1;
+        g_path = (int)value;
+    }
+    else if (!strcmp(name, "nt")) g_nt = (int)value;
+    else if (!strcmp(name, "dyn")) g_dyn = (int)value;
+    else if (!strcmp(name, "unroll")) {
+        if (value != 2 && value != 4 && value != 8) return -1;
+        g_unroll = (int)value;
+    }
+    else if (!strcmp(name, "blocks_per_cu")) g_bpc = (int)value;
     else if (!strcmp(name, "host_chunk_mb") && value > 0) ws_host_chunk_bytes = (size_t)value << 20;
     else if (!strcmp(name, "piece_scan")) ws_piece_scan = (int)value;
     else if (!strcmp(name, "reasm_path")) ws_reasm_path = (int)value;
@@ -111,8 +119,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
         *value = name[3] == 'n' ? ns : calls;
         return 0;
     }
-    if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks;
-    else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks;
+    if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks.load();
+    else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
     else return -1;
     return 0;
 }
@@ -274,12 +282,8 @@ static int decode_path(const WsTuning& t, u64 span, u32 nseg, u32 max_frames) {
 }
 
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
-    const WsTuning t = g_tune;
-    const int path = decode_path(t, span, nseg, max_frames);
-    if (path == 3) return ws_piece_workspace_bytes(span, nseg, max_frames);
-    if (path == 4) return 0;
-    if (path == 2) return (size_t)nseg * max_frames * 4 + (size_t)nseg * 4 + 256 + 256;
-    return 0;
+    const int path = decode_path(tuning(), span, nseg, max_frames);
+    return path == 3 ? ws_piece_workspace_bytes(span, nseg, max_frames) : 0;
 }
 
 int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, const u64* d_seg_len, u32 nseg,
@@ -293,7 +297,7 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
-    const WsTuning t = g_tune;
+    const WsTuning t = tuning();
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg; L.max_frames = max_frames;
     L.desc_base = d_desc_base; L.desc = d_desc; L.res = d_res;
@@ -301,7 +305,6 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     L.cus = ds->cus;
     u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
     const int path = decode_path(t, hi - lo, nseg, max_frames);
-    if (path == 0) return ws_launch_segblock(L, t.seg_cfg, t.nt);
     if (path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
     if (path == 4) return ws_launch_segfuse(L, t.nt);
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
@@ -309,30 +312,14 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     if (!ws && need) {
         if ((rc = workspace(ds, need, L.stream, &ws))) return rc;
     }
-    if (path == 3) {
-        const u32 gen = ws_next_gen();
-        const u32* disorder = nullptr;
-        // A/B tooling only: "debug" bit 3 reruns K2 on the previous call's scan (same batch)
-        static bool s_scanned = false;
-        if ((ws_dbg_flags & 8) && s_scanned) {
-            PieceWs P;
-            extern int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, PieceWs* out);
-            if ((rc = ws_piece_rescan_views(L, lo, hi, reinterpret_cast<unsigned char*>(ws), &P))) return rc;
-            extern int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
-            return ws_launch_piece_unmask(L, P, t.nt, gen);
-        }
-        s_scanned = true;
-        bool fallback = false;
-        if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder, &fallback)))
-            return rc;
-        // segments out of buffer order are decoded by K2's fallback; with no pieces to launch K2
-        // on, a small gated walker grid does it (exits at once for ordered batches)
-        return fallback ? ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen) : 0;
-    }
-    const size_t nslots = (size_t)nseg * max_frames;
-    u32* keys = reinterpret_cast<u32*>(ws);
-    u32* nwork = keys + ((nslots + 63) & ~(size_t)63);
-    return ws_launch_split(L, t.split_cfg, t.nt, keys, nwork);
+    const u32 gen = ws_next_gen();
+    const u32* disorder = nullptr;
+    bool fallback = false;
+    if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder, &fallback)))
+        return rc;
+    // segments out of buffer order are decoded by K2's fallback; with no pieces to launch K2
+    // on, a small gated walker grid does it (exits at once for ordered batches)
+    return fallback ? ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen) : 0;
 }
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, unsigned long long buflen,

@@ -1,10 +1,23 @@
-// ws_diag.hip — bench/test support kernels (not the decode path):
+// ws_bench.hip — libwsframe_amd_bench.so, bench/test support kernels (NOT part of the
+// drop-in libwsframe_amd.so; include/wsframe_amd_bench.h):
 //   * synthetic frame batches generated in HBM (ws_synth.h), and their verification;
 //   * streaming-bandwidth calibration kernels (the ceilings DESIGN.md §4 quotes).
 #include <stdio.h>
 
 #include "ws_common.h"
 #include "ws_synth.h"
+#include "../../include/wsframe_amd_bench.h"
+
+static __thread char g_bench_error[256];
+int ws_set_err(const char* what, hipError_t e) {
+    snprintf(g_bench_error, sizeof(g_bench_error), "%s: %s", what, hipGetErrorString(e));
+    return -(int)(e ? e : 1);
+}
+int ws_set_msg(const char* msg) {
+    snprintf(g_bench_error, sizeof(g_bench_error), "%s", msg);
+    return -1;
+}
+extern "C" WSFRAME_AMD_EXPORT const char* websocketframeBenchLastError(void) { return g_bench_error; }
 
 // ---------------------------------------------------------------------------------------------
 // synthetic batches (bench/test input; ws_synth.h)

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/wsframe_amd.h"
 
 typedef unsigned long long u64;
@@ -288,6 +290,9 @@ __device__ __forceinline__ bool ws_round_advance(const WsRound& r, u64& off, u64
 }
 
 // host side
+// a launch-tuning option (websocketframeGpuSetOption): atomic, so concurrent calls and
+// SetOption never race; each launcher reads the knobs it needs once per call
+typedef std::atomic<int> WsOpt;
 int ws_set_err(const char* what, hipError_t e);
 int ws_set_msg(const char* msg);
 
@@ -327,8 +332,6 @@ int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, cons
                     u32 max_frames, const u64* desc_base, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res,
                     hipStream_t stream, void* ws = nullptr, size_t ws_bytes = 0);
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
-int ws_launch_split(const WsLaunch& L, int variant, int nt, u32* keys, u32* nwork);
-int ws_launch_segblock(const WsLaunch& L, int cfg, int nt);
 int ws_launch_segfuse(const WsLaunch& L, int nt);
 bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
 
@@ -336,4 +339,4 @@ bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
 // (block b takes item (b & 1) * half + b / 2; half = 0 keeps b): two distant address
 // windows in flight beat one compact window on this HBM (tools/exp_win.sh).
 __device__ __forceinline__ u32 ws_win2(u32 b, u32 half) { return half ? (b & 1u) * half + (b >> 1) : b; }
-extern int ws_seg_win;
+extern WsOpt ws_seg_win;

@@ -362,10 +362,10 @@ static int enc_side(EncSide** out) {
     *out = &S;
     return 0;
 }
-int ws_encode_fused = 0;  // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
+WsOpt ws_encode_fused{0}; // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
                           // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
-int ws_enc_win = 0;       // "enc_win": E3 takes output pieces in two windows (ws_win2; measured 1 % slower)
-int ws_encode_side = 0;   // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
+WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (ws_win2; measured 1 % slower)
+WsOpt ws_encode_side{0};  // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
                           // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,

@@ -36,7 +36,7 @@ struct WsHostPipe {
 };
 static WsHostPipe g_pipe[WS_HOST_DEV];
 
-size_t ws_host_chunk_bytes = 64ull << 20;  // group size target ("host_chunk_mb")
+std::atomic<size_t> ws_host_chunk_bytes{64ull << 20};  // group size target ("host_chunk_mb")
 
 template <typename T>
 static int grow(T** p, size_t* cap, size_t need, const char* what) {

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
 // its items, descriptors and piece pointers are written by the lanes in parallel.
 // Small G keeps more segments in flight per wave (the walk is latency-bound).
 #define PSCAN_T 256
-template <int G, int DBG = 0>
+template <int G>
 __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned char* __restrict__ buf,
                                                                 const u64* __restrict__ seg_off,
                                                                 const u64* __restrict__ seg_len, u32 nseg,
@@ -184,12 +184,9 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
         if (gl < ntake) {                                                   // consumed frames, in parallel
-            if (!(DBG & 4)) {
-                put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0,
-                         rotl32(h.key, 8u * (u32)(p0 & 3)));
-                put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
-            }
-            if (!(DBG & 2) && h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
+            put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0, rotl32(h.key, 8u * (u32)(p0 & 3)));
+            put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
+            if (h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
         }
         const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
         if (ntake) walked_end = fe_last;
@@ -380,11 +377,10 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 
 // Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *disorder_out = the word a gated
 // fallback walker compares with `gen`.
-extern int ws_dbg_flags;
-int ws_piece_scan = 3;  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
+WsOpt ws_piece_scan{3};  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
 
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
-int ws_scan_win = 0;      // "scan_win": K1 takes its segment groups in two windows (ws_win2)
+WsOpt ws_scan_win{0};    // "scan_win": K1 takes its segment groups in two windows (ws_win2)
 
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
@@ -400,16 +396,13 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     P.nwork = reinterpret_cast<u32*>(ws + b);
     b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
     P.items = reinterpret_cast<u32x4*>(ws + b);
-    if (ws_piece_scan >= 1 && ws_piece_scan <= 4) {
-        const int G = ws_piece_scan == 1 ? 64 : (ws_piece_scan == 2 ? 32 : (ws_piece_scan == 3 ? 16 : 8));
+    const int scan = ws_piece_scan;
+    if (scan >= 1 && scan <= 4) {
+        const int G = scan == 1 ? 64 : (scan == 2 ? 32 : (scan == 3 ? 16 : 8));
         const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
         const u32 half = ws_scan_win && blocks >= 512 ? (blocks + 1) / 2 : 0;
         auto k = G == 64 ? ws_piece_scan_kernel<64>
                          : (G == 32 ? ws_piece_scan_kernel<32> : (G == 16 ? ws_piece_scan_kernel<16> : ws_piece_scan_kernel<8>));
-        // A/B tooling only (results wrong): "debug" bit 1 skips descriptor stores, bit 2 items + pointers
-        if (G == 16 && (ws_dbg_flags & 6))
-            k = (ws_dbg_flags & 6) == 2 ? ws_piece_scan_kernel<16, 2>
-                                        : ((ws_dbg_flags & 6) == 4 ? ws_piece_scan_kernel<16, 4> : ws_piece_scan_kernel<16, 6>);
         hipLaunchKernelGGL(k, dim3(half ? 2 * half : blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
                            L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
                            P.disorder, gen, P.pbase, lo, hi, half);
@@ -424,38 +417,19 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     return 0;
 }
 
-// the workspace views of an already scanned batch (A/B tooling: K2 without K1)
-int ws_piece_rescan_views(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, PieceWs* out) {
-    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
-    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
-    PieceWs P;
-    P.npieces = piece_count(lo_org, hi_org);
-    P.pbase = lo_org >> PIECE_SHIFT;
-    P.c_lo = lo_org >> 4;
-    P.c_hi = (hi_org + 15) >> 4;
-    P.disorder = reinterpret_cast<u32*>(ws);
-    P.ptr = reinterpret_cast<u64*>(ws + 16);
-    size_t b = (16 + P.npieces * 8 + 15) & ~(size_t)15;
-    P.nwork = reinterpret_cast<u32*>(ws + b);
-    b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
-    P.items = reinterpret_cast<u32x4*>(ws + b);
-    *out = P;
-    return 0;
-}
-
 // K2 alone over the pieces of a scanned batch
-int ws_piece_whole = 2;   // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
+WsOpt ws_piece_whole{2}; // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
-int ws_piece_occ = 0;     // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
-int ws_piece_wn = 0;      // "piece_wn": >= 2 windows of any count (overrides piece_win/piece_wbit)
-int ws_piece_wbit = 0;    // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
-int ws_piece_win = 1;     // "piece_win": log2 of the number of piece windows K2 streams side by side
+WsOpt ws_piece_occ{0};   // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
+WsOpt ws_piece_wn{0};    // "piece_wn": >= 2 windows of any count (overrides piece_win/piece_wbit)
+WsOpt ws_piece_wbit{0};  // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
+WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
 // "k2_timing" (measurement only, bench.py): a pair of HIP events is recorded around every
 // K2 launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
 // recorded K2 durations, "k2_calls" counts them; setting the option clears the record.
-int ws_k2_timing = 0;
+WsOpt ws_k2_timing{0};
 static std::vector<hipEvent_t> g_k2ev;    // start, end, start, end, ...
 static size_t g_k2n = 0;
 static std::mutex g_k2mu;
@@ -498,19 +472,19 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
     if (!P.npieces) return 0;
     size_t tslot = 0;
     int rc;
-    if (ws_k2_timing && (rc = k2_mark(L.stream, false, &tslot))) return rc;
-    auto k = nt == 1 ? (ws_piece_whole == 2 ? ws_piece_unmask_kernel<1, 2, 1>
-                                            : (ws_piece_whole == 1 ? ws_piece_unmask_kernel<1, 1, 1>
-                                                                   : ws_piece_unmask_kernel<1, 0, 1>))
-                     : (ws_piece_whole == 2 ? ws_piece_unmask_kernel<0, 2, 1>
-                                            : (ws_piece_whole == 1 ? ws_piece_unmask_kernel<0, 1, 1>
-                                                                   : ws_piece_unmask_kernel<0, 0, 1>));
-    if (ws_piece_occ == 7 || ws_piece_occ == 8)           // forced occupancy: spills, measured slower
-        k = ws_piece_occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
-    u32 wshift = (u32)(ws_piece_win < 0 ? 0 : (ws_piece_win > 6 ? 6 : ws_piece_win));
+    const int timing = ws_k2_timing, whole = ws_piece_whole, occ = ws_piece_occ;
+    const int pwin = ws_piece_win, pwbit = ws_piece_wbit, pwn = ws_piece_wn;
+    if (timing && (rc = k2_mark(L.stream, false, &tslot))) return rc;
+    auto k = nt == 1 ? (whole == 2 ? ws_piece_unmask_kernel<1, 2, 1>
+                                   : (whole == 1 ? ws_piece_unmask_kernel<1, 1, 1> : ws_piece_unmask_kernel<1, 0, 1>))
+                     : (whole == 2 ? ws_piece_unmask_kernel<0, 2, 1>
+                                   : (whole == 1 ? ws_piece_unmask_kernel<0, 1, 1> : ws_piece_unmask_kernel<0, 0, 1>));
+    if (occ == 7 || occ == 8)                              // forced occupancy: spills, measured slower
+        k = occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
+    u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
-    const u32 wbit = wshift ? (u32)(ws_piece_wbit < 0 ? 0 : (ws_piece_wbit > 8 ? 8 : ws_piece_wbit)) : 0u;
-    const u32 wn = ws_piece_wn >= 2 && (P.npieces / (u64)ws_piece_wn) >= 256 ? (u32)ws_piece_wn : 0u;
+    const u32 wbit = wshift ? (u32)(pwbit < 0 ? 0 : (pwbit > 8 ? 8 : pwbit)) : 0u;
+    const u32 wn = pwn >= 2 && (P.npieces / (u64)pwn) >= 256 ? (u32)pwn : 0u;
     const u64 ppw = wn ? (P.npieces + wn - 1) / wn
                        : (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
     const u64 grid = wn ? ppw * wn : ppw << wshift;
@@ -519,7 +493,7 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
                        L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces, wn);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
-    return ws_k2_timing ? k2_mark(L.stream, true, &tslot) : 0;
+    return timing ? k2_mark(L.stream, true, &tslot) : 0;
 }
 
 // K1 + K2; K2 also holds the fallback for unordered batches. *fallback_needed: no K2

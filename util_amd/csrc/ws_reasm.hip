@@ -17,7 +17,23 @@
 //    phase; the <=15 bytes at each body edge by byte ops (bodies are adjacent, so two
 //    waves may share an output chunk but never a byte).
 // The wire buffer is only read.
+//
+// Fragment-cache limit (websocketframeBatchReassembleDeviceEx): the stream hook refuses to
+// cache a body that would take the connection's cached bytes past readcache_max_size
+// (check_cache_overflow, net_channel_ex.c:45-53, applied at :129-135 to every frame that is
+// cached: one arriving while a message is pending, or a non-FIN one); the channel is then
+// detached with NET_REACTOR_CACHE_READ_OVERFLOW_ERR and the frame is not consumed. Both paths
+// stop the segment there with WEBSOCKET_SEG_ERR_CACHE_OVERFLOW (descriptor written, not
+// consumed, no body). Cached bytes are counted in u32 as the reference's
+// StreamTransportCtx_t.cache_recv_bytes (transport_ctx.c:179-201) and carried across batches.
 #include "ws_common.h"
+
+// check_cache_overflow (net_channel_ex.c:45-53) on u32 counts
+__device__ __forceinline__ bool ws_cache_overflow(u32 already, u32 add, u32 max_limit) {
+    if (max_limit == 0) return false;
+    if (max_limit < add) return true;
+    return already > max_limit - add;
+}
 
 #define RLAY_T 256
 #define RGAT_T 256
@@ -39,7 +55,7 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
     const u64* __restrict__ seg_len, const WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     const u32x4* __restrict__ items, const unsigned char* __restrict__ out, const u64* __restrict__ out_off,
     WebsocketMsgDesc_t* __restrict__ msg, u32* __restrict__ nmsg, unsigned char* __restrict__ open_io,
-    GatherRec* __restrict__ recs, u32* __restrict__ nbody) {
+    GatherRec* __restrict__ recs, u32* __restrict__ nbody, u32 cache_max, u32* __restrict__ cached_io) {
     constexpr u32 G = RLAY_G;
     const u32 lane = threadIdx.x & 63, gl = lane % G, gb = lane - gl;
     const u32 s = (blockIdx.x * RLAY_T + threadIdx.x) / G;
@@ -52,9 +68,11 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
     const u32 nf = active ? res[sc].n_frames : 0u;
     const int status0 = res[sc].status;
     u32 open = active && open_io ? open_io[sc] : 0u, cont = open;
+    u32 cached = open && cached_io ? cached_io[sc] : 0u;                     // bytes of the pending message
     u32 nm = 0, nb = 0, first = 0;                                           // group-uniform state
     u64 q = 0, q0 = 0;
     bool stop = false, overflow = false;
+    int cstop_frame = -1;                                                    // frame refused by the cache limit
     const u64 gmask = (1ull << G) - 1;
     (void)buf;
     for (u32 k0 = 0; __ballot(active && !stop && k0 < nf); k0 += G) {
@@ -79,7 +97,29 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
         const u64 qs = q + incl - len;                                       // this body's output offset
         // bodies must fit the segment's region (only the (int) return quirk can break this)
         const u64 ovm = (__ballot(body && len > sl - qs) >> gb) & gmask;   // qs <= sl before the first overflow
-        const u32 ntake = ovm ? (u32)__builtin_ctzll(ovm) : nbody_r;
+        u32 ntake = ovm ? (u32)__builtin_ctzll(ovm) : nbody_r;
+        // the fragment cache's limit: pending before frame k = frame k-1 was not FIN (lane 0: the
+        // carried state); cached bytes before k = the current message's bodies before k (u32)
+        const u32 blen = (u32)len;
+        u32 cincl = blen;
+#pragma unroll
+        for (u32 o = 1; o < G; o <<= 1) {
+            const u32 t = (u32)__shfl_up((int)cincl, o, G);
+            if (gl >= o) cincl += t;
+        }
+        const bool finb = body && d.is_fin;
+        const u64 fin_all = (__ballot(finb) >> gb) & gmask;
+        const u64 fin_below = fin_all & ((1ull << gl) - 1);
+        const u32 lastf = fin_below ? 63 - __builtin_clzll(fin_below) : 0;
+        const u32 cincl_lastf = (u32)__shfl((int)cincl, (int)(gb + lastf), 64);
+        const u32 cbefore = fin_below ? cincl - blen - cincl_lastf : cached + cincl - blen;
+        const bool pend = gl == 0 ? open != 0 : !((fin_all >> (gl - 1)) & 1ull);
+        const u64 ccm = (__ballot(body && (pend || !d.is_fin) && ws_cache_overflow(cbefore, blen, cache_max)) >> gb) & gmask;
+        const u32 cst = ccm ? (u32)__builtin_ctzll(ccm) : 64u;
+        if (cst < ntake) {
+            ntake = cst;
+            cstop_frame = (int)(k0 + cst);
+        }
         if (gl < ntake) {
             const u64 p0 = ((u64)it.x | ((u64)it.y << 32)) & 0xFFFFFFFFFFFFull;
             const u32 rk = (u32)(((u64)it.x | ((u64)it.y << 32)) >> 48) | ((u32)(((u64)it.z | ((u64)it.w << 32)) >> 48) << 16);
@@ -107,6 +147,9 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
         const u32 last = finm ? 63 - __builtin_clzll(finm) : 0;             // last FIN of the round
         const u64 incl_last = __shfl(incl, (int)(gb + last), 64);
         const u64 tot = ntake ? tot_l : 0;
+        const u32 ctot = (u32)__shfl((int)cincl, (int)(gb + (ntake ? ntake - 1 : 0)), 64);
+        const u32 clast = (u32)__shfl((int)cincl, (int)(gb + last), 64);
+        if (ntake) cached = finm ? (ntake > last + 1 ? ctot - clast : 0u) : cached + ctot;
         if (finm) {
             q0 = q + incl_last;
             first = k0 + last + 1;
@@ -119,7 +162,7 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
         q += tot;
         nb += ntake;
         if (ntake < G || k0 + G >= nf) stop = true;                          // error frame, overflow or end
-        if (ovm) overflow = true;
+        if (ovm && cstop_frame < 0) overflow = true;
         if (!active) stop = true;
     }
     if (!active || gl != 0) return;
@@ -129,11 +172,17 @@ __global__ __launch_bounds__(RLAY_T) void ws_reasm_layout_kernel(
         m.complete = 0; m.continued = cont;
         msg[base + nm++] = m;
     }
-    if (overflow) res[s].status = WEBSOCKET_SEG_ERR_OUT_SPACE;
+    if (cstop_frame >= 0) {                                                  // not consumed; the channel detaches
+        const WebsocketFrameDesc_t dc = desc[base + (u32)cstop_frame];
+        ws_store_res(res + s, dc.frame_off - so, (u32)cstop_frame + 1, WEBSOCKET_SEG_ERR_CACHE_OVERFLOW);
+    } else if (overflow) {
+        res[s].status = WEBSOCKET_SEG_ERR_OUT_SPACE;
+    }
     (void)status0;
     nmsg[s] = nm;
     nbody[s] = nb;
     if (open_io) open_io[s] = (unsigned char)open;
+    if (cached_io) cached_io[s] = open ? cached : 0u;
 }
 
 typedef u32x4 __attribute__((aligned(1))) u32x4u;
@@ -232,7 +281,8 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
     const u64* __restrict__ seg_len, WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     unsigned char* __restrict__ out, const u64* __restrict__ out_off, WebsocketMsgDesc_t* __restrict__ msg,
-    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io, u32 merge, u32 nseg, u32 half) {
+    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io, u32 merge, u32 nseg, u32 half, u32 cache_max,
+    u32* __restrict__ cached_io) {
     constexpr u32 RSEG_C = (RSEG_L - 1) * 64;         // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[RSEG_L * 64];
     __shared__ BodyL tab[RSEG_TB];
@@ -258,6 +308,7 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     int status = WEBSOCKET_SEG_OK;
     bool walking = true, bodies_on = true, overflow = false;
     u32 open = w0 && open_io ? open_io[s] : 0u, cont = open;
+    u32 cached = open && cached_io ? cached_io[s] : 0u;             // bytes of the pending message (u32)
     u64 wc = 0;                                                      // window's first chunk
     for (;;) {
         const u64 W0 = wc << 4, W1 = W0 + (u64)RSEG_C * 16;
@@ -294,8 +345,28 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
                     const u64 qs = q + incl - len;
                     // bodies must fit the segment's region (qs <= sl for every lane before the first overflow)
                     const u64 ovm = __ballot(body && len > sl - qs);
-                    const u32 ntb = ovm ? (u32)__builtin_ctzll(ovm) : nbr;
-                    if (ovm) { bodies_on = false; overflow = true; }
+                    u32 ntb = ovm ? (u32)__builtin_ctzll(ovm) : nbr;
+                    // the fragment cache's limit (see the file header): pending before lane i =
+                    // frame i-1 not FIN (lane 0: carried), cached bytes = the message's bodies so far
+                    const u32 blen = (u32)len;
+                    u32 cincl = blen;
+#pragma unroll
+                    for (u32 d = 1; d < 64; d <<= 1) {
+                        const u32 t = (u32)__shfl_up((int)cincl, d, 64);
+                        if (lane >= d) cincl += t;
+                    }
+                    const bool finl = h.b0 >> 7;
+                    const u64 fin_all = __ballot(body && finl);
+                    const u64 fin_below = fin_all & ((1ull << lane) - 1);
+                    const u32 lastf = fin_below ? 63 - __builtin_clzll(fin_below) : 0;
+                    const u32 cincl_lastf = (u32)__shfl((int)cincl, (int)lastf, 64);
+                    const u32 cbefore = fin_below ? cincl - blen - cincl_lastf : cached + cincl - blen;
+                    const bool pend = lane == 0 ? open != 0 : !((fin_all >> (lane - 1)) & 1ull);
+                    const u64 ccm = __ballot(body && (pend || !finl) && ws_cache_overflow(cbefore, blen, cache_max));
+                    const u32 cst = ccm ? (u32)__builtin_ctzll(ccm) : 64u;
+                    const bool cref = cst < ntb;                 // refused before any out-of-space body
+                    if (cref) ntb = cst;
+                    else if (ovm) { bodies_on = false; overflow = true; }
                     if (lane < ntb) {
                         BodyL b;
                         b.x0 = X + h.hdr; b.dst = qs; b.len = len;
@@ -328,8 +399,18 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
                     } else if (ntb) {
                         open = 1;
                     }
+                    const u32 ctot = (u32)__shfl((int)cincl, (int)(ntb ? ntb - 1 : 0), 64);
+                    const u32 clast = (u32)__shfl((int)cincl, (int)last, 64);
+                    if (ntb) cached = finm ? (ntb > last + 1 ? ctot - clast : 0u) : cached + ctot;
                     q += ntb ? tot : 0;
                     nb += ntb;
+                    if (cref) {                              // refused: not consumed, the walk ends there
+                        off = __shfl(pos, (int)cst, 64);
+                        nf += cst + 1;
+                        status = WEBSOCKET_SEG_ERR_CACHE_OVERFLOW;
+                        walking = false;
+                        break;
+                    }
                 }
                 if (!ws_round_advance(r, off, g, nf, status, walking)) break;
             }
@@ -433,21 +514,22 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     ws_store_res(res + s, off, nf, overflow ? WEBSOCKET_SEG_ERR_OUT_SPACE : status);
     nmsg[s] = nm;
     if (open_io) open_io[s] = (unsigned char)open;
+    if (cached_io) cached_io[s] = open ? cached : 0u;
 }
 
 // 0 auto, 1 fused segment kernel, 2 scan + layout + gather ("reasm_path")
-int ws_reasm_path = 0;
+WsOpt ws_reasm_path{0};
 // fused kernel geometry ("reasm_cfg"): 0 17 KiB windows + 8 waves/SIMD (SGPR spills: slower),
 // 1 17 KiB windows at the compiler's occupancy (7 waves/SIMD, default), 2 19 KiB windows
-int ws_reasm_cfg = 1;
-int ws_reasm_merge = 0;   // "reasm_merge": 1 body-boundary chunks assembled whole by one lane, 0 one
+WsOpt ws_reasm_cfg{1};
+WsOpt ws_reasm_merge{0}; // "reasm_merge": 1 body-boundary chunks assembled whole by one lane, 0 one
                           // byte-store instruction from 31 lanes (default: measured faster, cfg5u 1.50 vs 1.65 ms)
 
-extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
     unsigned int nseg, unsigned int max_frames, WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
     unsigned char* d_out, const u64* d_out_off, WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
-    unsigned char* d_open, void* hip_stream) {
+    unsigned char* d_open, unsigned int readcache_max_size, unsigned int* d_cached, void* hip_stream) {
     if (nseg == 0) return 0;
     if (!d_buf || !d_seg_off || !d_seg_len || !d_desc || !d_res || !d_out || !d_msg || !d_nmsg || max_frames == 0)
         return ws_set_msg("websocketframeBatchReassembleDevice: invalid argument");
@@ -456,15 +538,14 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     // fused segment kernel for many small segments (one-shot blocks); the three-kernel
     // path for few or large segments (its gather spreads one segment over many waves)
-    const bool fused = ws_reasm_path == 1 ||
-                       (ws_reasm_path == 0 && max_frames <= RSEG_TB && nseg >= 1024 && buflen <= (u64)nseg << 18);
+    const int rpath = ws_reasm_path, rcfg = ws_reasm_cfg;
+    const bool fused = rpath == 1 || (rpath == 0 && max_frames <= RSEG_TB && nseg >= 1024 && buflen <= (u64)nseg << 18);
     if (fused && max_frames <= RSEG_TB) {
-        auto k = ws_reasm_cfg == 1 ? ws_reasm_seg_kernel<18, 1>
-                                   : (ws_reasm_cfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
+        auto k = rcfg == 1 ? ws_reasm_seg_kernel<18, 1> : (rcfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
         const u32 half = ws_seg_win && nseg >= 512 ? (nseg + 1) / 2 : 0;
         hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
                            d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, (u32)ws_reasm_merge,
-                           nseg, half);
+                           nseg, half, (u32)readcache_max_size, d_cached);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);
     }
@@ -485,7 +566,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
     if ((rc = ws_launch_piece_scan(L, 0, buflen, w8, ws_next_gen(), &P))) return rc;
     hipLaunchKernelGGL(ws_reasm_layout_kernel, dim3((u32)(((u64)nseg * RLAY_G + RLAY_T - 1) / RLAY_T)), dim3(RLAY_T), 0, st, d_buf, nseg,
                        max_frames, d_seg_off, d_seg_len, d_desc, d_res, P.items, d_out, d_out_off, d_msg, d_nmsg,
-                       d_open, recs, nbody);
+                       d_open, recs, nbody, (u32)readcache_max_size, d_cached);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_reasm_layout_kernel launch", e);
     const u64 waves = nslots;
@@ -495,4 +576,13 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
                        recs, nbody);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_reasm_gather_kernel launch", e);
     return 0;
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDevice(
+    const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
+    unsigned int nseg, unsigned int max_frames, WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
+    unsigned char* d_out, const u64* d_out_off, WebsocketMsgDesc_t* d_msg, unsigned int* d_nmsg,
+    unsigned char* d_open, void* hip_stream) {
+    return websocketframeBatchReassembleDeviceEx(d_buf, buflen, d_seg_off, d_seg_len, nseg, max_frames, d_desc, d_res,
+                                                 d_out, d_out_off, d_msg, d_nmsg, d_open, 0, nullptr, hip_stream);
 }

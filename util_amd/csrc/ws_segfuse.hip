@@ -161,7 +161,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
     if (tid == 0) ws_store_res(res + s, off, nf, status);
 }
 
-int ws_segfuse_cfg = 0;   // "segfuse_cfg": 0 256 threads, 17 KiB windows (8 workgroups/CU), 1 256 x 19 KiB,
+WsOpt ws_segfuse_cfg{0}; // "segfuse_cfg": 0 256 threads, 17 KiB windows (8 workgroups/CU), 1 256 x 19 KiB,
                           // 2 1024 x 65 KiB (one window per 64 KiB segment), 3 512 x 33 KiB
 
 int ws_launch_segfuse(const WsLaunch& L, int nt) {

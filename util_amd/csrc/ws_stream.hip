@@ -493,11 +493,10 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
 
 #define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
 #define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
-int ws_stream_rw = 1;            // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
-int ws_stream_rw_cmax = 23;      // "stream_rw_cmax": log2 of the largest chunk
-extern int ws_dbg_flags;
-unsigned long long ws_stat_rw_chunks = 0;       // chunks written from records (last call)
-unsigned long long ws_stat_rw_chunk_walks = 0;  // chunks walked by one wavefront without a record
+WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
+WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
+std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
+std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
 
 // grow-only scratch for the chunk-parallel walk (per device): device records + counters,
 // and a pinned host copy of them
@@ -633,11 +632,9 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
                        need_mask, cand, capc, recs, nrec, dx);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
-    if (!(ws_dbg_flags & 128)) {                                             // A/B: window walks only
-        hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
-                           P, C, (u32)nchunks, need_mask, dx, own, stg, stgn);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
-    }
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len, P,
+                       C, (u32)nchunks, need_mask, dx, own, stg, stgn);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return ws_set_err("stream walk records", e);
@@ -693,10 +690,6 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
             ent = ow->exit;
             continue;
         }
-        if ((ws_dbg_flags & 16) && ws_stat_rw_chunk_walks < 6 && c < nchunks)
-            fprintf(stderr, "rw: chunk %llu/%llu C %llu H %u entry +%llu n0 %u n1 %u A %d owner %d\n",
-                    (unsigned long long)c, (unsigned long long)nchunks, (unsigned long long)C, H,
-                    (unsigned long long)(ent - cs0), hn[4 * c], hn[4 * c + 1], r ? 1 : 0, oi != ~0ull ? 1 : 0);
         u64 nx = 0;
         u32 nfn = 0;
         if ((rc = chunk_walk(ent, nfc, cs0 + C, nx, nfn)) < 0) return rc;
@@ -705,24 +698,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         nfc = nfn;
     }
     const u32 nblk = (u32)(ht.size() / 8);
-    if (ws_dbg_flags & 64)
-        fprintf(stderr, "rw: chain of %u chunks resolved in %.1f us\n", (unsigned)(ht.size() / 8),
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_rec).count());
     ws_stat_rw_chunks = nblk;
-    if (ws_dbg_flags & 32) {
-        fprintf(stderr, "rw: len %llu P %llu C %llu H %u nchunks %llu\n", (unsigned long long)len,
-                (unsigned long long)P, (unsigned long long)C, H, (unsigned long long)nchunks);
-        for (u32 i = 0; i < nblk; ++i) {
-            const u64* t = ht.data() + 8 * i;
-            fprintf(stderr, "rw: row %u ent %llu exit_w %llu nf0 %llu cnt_w %llu oi %lld n_par %llu last %llu", i,
-                    (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2],
-                    (unsigned long long)t[3], (long long)t[4], (unsigned long long)t[5], (unsigned long long)t[6]);
-            if (t[4] != ~0ull)
-                fprintf(stderr, " own exit %llu cs %x dead %u", (unsigned long long)hown[t[4]].exit, hown[t[4]].cs,
-                        hown[t[4]].dead);
-            fprintf(stderr, "\n");
-        }
-    }
     if (nblk) {
         if ((e = hipMemcpyAsync(tab, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stream chain)", e);

@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import WsDesc, WsSegRes, check, load_lib
+from ._lib import WsDesc, WsSegRes, check, check_bench, load_bench_lib, load_lib
 
 WEBSOCKET_CONTINUE_FRAME = 0
 WEBSOCKET_TEXT_FRAME = 1
@@ -22,6 +22,8 @@ WEBSOCKET_MAX_ENCODE_HEADLENGTH = 10
 
 SEG_OK, SEG_MAX_FRAMES, SEG_ERR_DECODE, SEG_ERR_LEN_WRAP = 0, 1, -1, -2
 SEG_ERR_OUT_SPACE = -3
+SEG_ERR_CACHE_OVERFLOW = -4
+NETPACKET_FRAGMENT = 6  # transport_ctx.h:11-18; the pktype websocketframeOnDecode reports
 DATA_OFF_NULL = 0xFFFFFFFFFFFFFFFF
 BATCH_PAD = 32  # WEBSOCKET_BATCH_PAD: readable device bytes required after every segment
 
@@ -137,6 +139,8 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
     nseg = seg_off.numel()
     assert buf.numel() >= BATCH_PAD, "device batch needs WEBSOCKET_BATCH_PAD bytes of slack"
     assert seg_len.numel() == nseg and res.numel() * res.element_size() >= 16 * nseg
+    if desc_base is None:
+        assert desc.numel() * desc.element_size() >= 32 * nseg * max_frames, "desc holds < nseg*max_frames slots"
     assert buf.is_cuda and seg_off.is_cuda and seg_len.is_cuda and desc.is_cuda and res.is_cuda
     # buflen: segments lie in [0, numel - PAD); the last PAD bytes are the readable slack
     rc = load_lib().websocketframeBatchDecodeDevice(_ptr(buf), buf.numel() - BATCH_PAD, _ptr(seg_off), _ptr(seg_len),
@@ -155,17 +159,24 @@ def stream_decode_device(buf, length, max_frames, desc, res, stream=None):
 
 
 def batch_reassemble_device(buf, seg_off, seg_len, max_frames, desc, res, out, msg, nmsg, out_off=None, open_state=None,
-                            stream=None):
-    """websocketframeBatchReassembleDevice on torch CUDA tensors: buf (uint8, wire, read only;
+                            stream=None, readcache_max=0, cached=None):
+    """websocketframeBatchReassembleDeviceEx on torch CUDA tensors: buf (uint8, wire, read only;
     the last BATCH_PAD bytes are slack), seg_off/seg_len/out_off (int64), desc (uint8
     >= 32*nseg*max_frames), res (uint8 16*nseg), out (uint8), msg (uint8 >= 32*nseg*max_frames),
-    nmsg (int32 nseg), open_state (uint8 nseg, in/out, optional); async on `stream`."""
+    nmsg (int32 nseg), open_state (uint8 nseg, in/out, optional), readcache_max (the channel's
+    readcache_max_size, 0 = unlimited), cached (int32 nseg, in/out, optional: the pending
+    message's cached bytes, u32); async on `stream`."""
     nseg = seg_off.numel()
     assert buf.numel() >= BATCH_PAD and seg_len.numel() == nseg and nmsg.numel() >= nseg
-    rc = load_lib().websocketframeBatchReassembleDevice(
+    assert desc.numel() * desc.element_size() >= 32 * nseg * max_frames
+    assert msg.numel() * msg.element_size() >= 32 * nseg * max_frames
+    assert res.numel() * res.element_size() >= 16 * nseg
+    assert cached is None or cached.numel() * cached.element_size() >= 4 * nseg
+    rc = load_lib().websocketframeBatchReassembleDeviceEx(
         _ptr(buf), buf.numel() - BATCH_PAD, _ptr(seg_off), _ptr(seg_len), nseg, max_frames, _ptr(desc), _ptr(res),
-        _ptr(out), _ptr(out_off), _ptr(msg), _ptr(nmsg), _ptr(open_state), _stream(stream))
-    check(rc, "websocketframeBatchReassembleDevice")
+        _ptr(out), _ptr(out_off), _ptr(msg), _ptr(nmsg), _ptr(open_state), int(readcache_max), _ptr(cached),
+        _stream(stream))
+    check(rc, "websocketframeBatchReassembleDeviceEx")
 
 
 def batch_encode_device(src, frames, dst, wire_off, capacity=None, stream=None):
@@ -196,15 +207,17 @@ def batch_decode_host(buf, seg_off, seg_len, max_frames, device=0):
 
 
 def synth_device(buf, frame_off, nframes, plen_kind, fixed_len, b0_kind, seed, stream=None):
-    rc = load_lib().websocketframeSynthDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, b0_kind,
-                                              seed, _stream(stream))
-    check(rc, "websocketframeSynthDevice")
+    """websocketframeSynthDevice (libwsframe_amd_bench.so): bench/test input, generated in HBM"""
+    rc = load_bench_lib().websocketframeSynthDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, b0_kind,
+                                                    seed, _stream(stream))
+    check_bench(rc, "websocketframeSynthDevice")
 
 
 def synth_verify_device(buf, frame_off, nframes, plen_kind, fixed_len, seed, expect_plain, mismatch, stream=None):
-    rc = load_lib().websocketframeSynthVerifyDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, seed,
-                                                    1 if expect_plain else 0, _ptr(mismatch), _stream(stream))
-    check(rc, "websocketframeSynthVerifyDevice")
+    rc = load_bench_lib().websocketframeSynthVerifyDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len,
+                                                          seed, 1 if expect_plain else 0, _ptr(mismatch),
+                                                          _stream(stream))
+    check_bench(rc, "websocketframeSynthVerifyDevice")
 
 
 def set_option(name, value):
