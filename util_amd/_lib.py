@@ -53,10 +53,22 @@ def build_lib(force=False):
     return LIB_PATH
 
 
+def _one_hip_runtime():
+    """Load torch (when installed) before our libraries: torch's ROCm wheel carries its own
+    libamdhip64 (soname libamdhip64.so.7, NEEDED as "libamdhip64.so"), so a library of ours
+    loaded first would pull /opt/rocm's copy in and the process would hold two HIP runtimes
+    (kernels of the second one then see no device). Loaded after torch, ours bind to torch's."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_lib():
     global _lib
     if _lib is not None:
         return _lib
+    _one_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libwsframe_amd.so not built: run __graft_entry__.build() "
                            "(make -C util_amd/csrc); there is no fallback path")
@@ -114,6 +126,7 @@ def load_bench_lib():
     global _bench
     if _bench is not None:
         return _bench
+    _one_hip_runtime()
     if not os.path.exists(BENCH_LIB_PATH):
         raise RuntimeError("libwsframe_amd_bench.so not built: run __graft_entry__.build()")
     lib = C.CDLL(BENCH_LIB_PATH)

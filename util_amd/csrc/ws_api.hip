@@ -31,7 +31,7 @@ extern WsOpt ws_piece_whole;
 extern WsOpt ws_piece_occ;
 extern WsOpt ws_piece_win;
 extern WsOpt ws_piece_wbit;
-extern WsOpt ws_k2_timing;
+extern WsOpt ws_k2_timing, ws_k2_probe;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_scan_win;
@@ -75,7 +75,7 @@ static WsTuning tuning() {                        // one consistent read per cal
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
     if (!strcmp(name, "path")) {
-        if (value != -1 && value != 1 && value != 3 && value != 4) return -1;
+        if (value != -1 && value != 1 && value != 3 && value != 4 && value != 5) return -1;
         g_path = (int)value;
     }
     else if (!strcmp(name, "nt")) g_nt = (int)value;
@@ -105,6 +105,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_k2_timing_reset();
     }
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
+    else if (!strcmp(name, "k2_probe")) ws_k2_probe = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
     else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
     else return -1;
@@ -135,12 +136,17 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
 #define WS_STREAM_SLOTS 16
 struct WsStreamWs {
     hipStream_t stream = nullptr;
-    bool captured = false;         // first used by a capturing stream: never reassigned
+    unsigned long long capture = 0; // capture id of the graph this slot belongs to (0: eager calls)
+    bool captured = false;         // belongs to a graph capture: never reassigned, never given to eager calls
     unsigned long long last = 0;   // LRU tick
     u32* ws = nullptr;             // decode / reassembly / stream workspace
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
+    void* sws = nullptr;           // path 5 workspace (ws_spec.hip), zeroed when allocated, never shared
+    size_t sws_bytes = 0;
+    u32 spec_calls = 0;            // path 5 calls on this slot (repair-count ring index)
+    u32* spec_host = nullptr;      // host-mapped: segments the last path 5 call repaired (~0u: none yet)
 };
 struct WsDevState {
     int init = 0;
@@ -177,30 +183,41 @@ static bool capturing(hipStream_t stream) {
     return hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
 }
 
-// the stream's workspace slot (caller holds g_dev_mu). Eager calls keep at most
-// WS_STREAM_SLOTS slots: a further stream takes the least recently used one after a
-// device synchronize. A stream capturing a graph cannot synchronize, so it always gets
-// a slot of its own (its graph keeps using that workspace on every replay).
+// the id of the capture the stream is in (0: not capturing)
+static unsigned long long capture_id(hipStream_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(stream, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return 0;
+    return id ? id : ~0ull;
+}
+
+// the workspace slot of (stream, capture) (caller holds g_dev_mu). Eager calls keep at most
+// WS_STREAM_SLOTS slots: a further stream takes the least recently used one after a device
+// synchronize. Every graph capture gets slots of its own, keyed by its capture id (torch
+// captures every graph on one shared stream, so the stream alone does not tell graphs apart):
+// its graph uses that workspace on every replay, so it is never handed to another capture or
+// to an eager call, and graphs captured separately may be replayed concurrently.
 static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
+    const unsigned long long cap = capture_id(stream);
     WsStreamWs* lru = nullptr;
     for (WsStreamWs& w : ds->sw) {
-        if (w.stream == stream) {
+        if (w.stream == stream && w.capture == cap) {
             w.last = ++ds->tick;
             *out = &w;
             return 0;
         }
         if (!w.captured && (!lru || w.last < lru->last)) lru = &w;
     }
-    const bool cap = capturing(stream);
     if (cap || ds->sw.size() < WS_STREAM_SLOTS || !lru) {
         ds->sw.emplace_back();
         lru = &ds->sw.back();
-        lru->captured = cap;
+        lru->captured = cap != 0;
     } else {                       // every slot taken by another stream: drain the device, then reuse
         hipError_t e = hipDeviceSynchronize();
         if (e != hipSuccess) return ws_set_err("hipDeviceSynchronize", e);
     }
     lru->stream = stream;
+    lru->capture = cap;
     lru->last = ++ds->tick;
     *out = lru;
     return 0;
@@ -210,7 +227,7 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
 // A stream capturing a graph (e.g. torch's private capture stream) may get its first
 // allocation (hipMalloc in relaxed capture mode, the head zeroed by a captured memset)
 // but cannot drain and free an existing one.
-static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, bool zero_head, const char* what) {
+static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, size_t zero_bytes, const char* what) {
     if (*have >= bytes) return 0;
     hipError_t e;
     const bool cap = capturing(stream);
@@ -228,7 +245,8 @@ static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, bool z
     e = hipMalloc(p, sz);
     if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
     if (e != hipSuccess) return ws_set_err(what, e);
-    if (zero_head && (e = hipMemsetAsync(*p, 0, 16, stream)) != hipSuccess) return ws_set_err(what, e);
+    if (zero_bytes && (e = hipMemsetAsync(*p, 0, zero_bytes < sz ? zero_bytes : sz, stream)) != hipSuccess)
+        return ws_set_err(what, e);
     *have = sz;
     return 0;
 }
@@ -239,7 +257,7 @@ static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream, void** ou
     int rc = stream_slot(ds, stream, &w);
     if (rc) return rc;
     void* p = w->ws;
-    if ((rc = grow(&p, &w->ws_bytes, bytes, stream, true, "hipMalloc(workspace)"))) return rc;
+    if ((rc = grow(&p, &w->ws_bytes, bytes, stream, 16, "hipMalloc(workspace)"))) return rc;
     w->ws = reinterpret_cast<u32*>(p);
     *out = p;
     return 0;
@@ -253,8 +271,38 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     WsStreamWs* w = nullptr;
     if ((rc = stream_slot(ds, stream, &w))) return rc;
-    if ((rc = grow(&w->ews, &w->ews_bytes, bytes, stream, false, "hipMalloc(encode workspace)"))) return rc;
+    if ((rc = grow(&w->ews, &w->ews_bytes, bytes, stream, 0, "hipMalloc(encode workspace)"))) return rc;
     *out = w->ews;
+    return 0;
+}
+
+// path 5 workspace (ws_spec.hip): its own allocation per slot, zeroed whole when allocated
+// (repair flags, count ring, disorder word); *call = this call's index on the slot;
+// *host = the slot's host-mapped repair count (written by the call's repair kernel)
+static int spec_workspace(WsDevState* ds, size_t bytes, hipStream_t stream, void** out, u32* call, u32** host,
+                          u32* last_repaired) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    WsStreamWs* w = nullptr;
+    int rc = stream_slot(ds, stream, &w);
+    if (rc) return rc;
+    if ((rc = grow(&w->sws, &w->sws_bytes, bytes, stream, ~(size_t)0, "hipMalloc(spec workspace)"))) return rc;
+    if (!w->spec_host) {
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        const bool cap = capturing(stream);
+        if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
+        void* h = nullptr;
+        const hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped);
+        if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
+        if (e != hipSuccess) return ws_set_err("hipHostMalloc(spec counter)", e);
+        w->spec_host = reinterpret_cast<u32*>(h);
+        *reinterpret_cast<volatile u32*>(w->spec_host) = ~0u;
+    }
+    *last_repaired = *reinterpret_cast<volatile u32*>(w->spec_host);
+    *out = w->sws;
+    *call = w->spec_calls++;
+    u32* dev_host = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_host), w->spec_host, 0) != hipSuccess) dev_host = nullptr;
+    *host = dev_host;
     return 0;
 }
 
@@ -277,6 +325,7 @@ int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
 // the decode variant a call takes
 static int decode_path(const WsTuning& t, u64 span, u32 nseg, u32 max_frames) {
     if (t.path == 4) return max_frames <= 64 ? 4 : 3;                 // segfuse holds <= 64 frames per segment
+    if (t.path == 5) return 5;
     if (t.path >= 0) return t.path;
     return ws_segfuse_fits(span, nseg, max_frames) ? 4 : 3;
 }
@@ -305,6 +354,15 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     L.cus = ds->cus;
     u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
     const int path = decode_path(t, hi - lo, nseg, max_frames);
+    if (path == 5) {
+        void* sws = nullptr;
+        u32 call = 0, last = 0;
+        u32* host = nullptr;
+        if ((rc = spec_workspace(ds, ws_spec_workspace_bytes(hi - lo, nseg), L.stream, &sws, &call, &host, &last)))
+            return rc;
+        (void)call;
+        return ws_launch_spec(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(sws), host);
+    }
     if (path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
     if (path == 4) return ws_launch_segfuse(L, t.nt);
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
