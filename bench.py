@@ -25,7 +25,7 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
-KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel", 5: "ws_spec_unmask_kernel"}
+KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel"}
 STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel (which decodes unordered batches itself, "
                    "one wave per segment)",
                 4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)"}
@@ -39,8 +39,6 @@ def decode_path(path, wl):
         path = int(opt["path"])
     if path == 4:
         return 4 if wl.fps <= 64 else 3
-    if path == 5:
-        return 5
     if path >= 0:
         return path
     return 4 if wl.fps <= 64 and wl.nseg >= 1024 and wl.wire_bytes <= wl.nseg * ((17 << 10) - 64) else 3

@@ -24,10 +24,9 @@ def dev():
     return torch.device("cuda:0")
 
 
-# decode variants: -1 auto (the default), 3 the piece path (scan kernel + one-shot 16 KiB
-# piece unmask), 4 one workgroup per segment (segfuse), 5 the predicted-chain path (ws_spec.hip:
-# prediction checked by the unmask blocks, mispredicted segments undone and walked exactly)
-@pytest.fixture(params=[-1, 3, 4, 5], ids=["auto", "piece", "segfuse", "spec"], autouse=True)
+# decode variants: -1 auto (the default: 4 for many small segments, else 3), 3 the piece
+# path (scan kernel + one-shot 16 KiB piece unmask), 4 one workgroup per segment (segfuse)
+@pytest.fixture(params=[-1, 3, 4], ids=["auto", "piece", "segfuse"], autouse=True)
 def decode_path(request):
     W.set_option("path", request.param)
     yield request.param

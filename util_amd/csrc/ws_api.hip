@@ -31,7 +31,7 @@ extern WsOpt ws_piece_whole;
 extern WsOpt ws_piece_occ;
 extern WsOpt ws_piece_win;
 extern WsOpt ws_piece_wbit;
-extern WsOpt ws_k2_timing, ws_k2_probe;
+extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_scan_win;
@@ -75,7 +75,7 @@ static WsTuning tuning() {                        // one consistent read per cal
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
     if (!strcmp(name, "path")) {
-        if (value != -1 && value != 1 && value != 3 && value != 4 && value != 5) return -1;
+        if (value != -1 && value != 1 && value != 3 && value != 4) return -1;
         g_path = (int)value;
     }
     else if (!strcmp(name, "nt")) g_nt = (int)value;
@@ -105,7 +105,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_k2_timing_reset();
     }
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
-    else if (!strcmp(name, "k2_probe")) ws_k2_probe = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
     else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
     else return -1;
@@ -143,10 +142,6 @@ struct WsStreamWs {
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
-    void* sws = nullptr;           // path 5 workspace (ws_spec.hip), zeroed when allocated, never shared
-    size_t sws_bytes = 0;
-    u32 spec_calls = 0;            // path 5 calls on this slot (repair-count ring index)
-    u32* spec_host = nullptr;      // host-mapped: segments the last path 5 call repaired (~0u: none yet)
 };
 struct WsDevState {
     int init = 0;
@@ -276,36 +271,6 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     return 0;
 }
 
-// path 5 workspace (ws_spec.hip): its own allocation per slot, zeroed whole when allocated
-// (repair flags, count ring, disorder word); *call = this call's index on the slot;
-// *host = the slot's host-mapped repair count (written by the call's repair kernel)
-static int spec_workspace(WsDevState* ds, size_t bytes, hipStream_t stream, void** out, u32* call, u32** host,
-                          u32* last_repaired) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    WsStreamWs* w = nullptr;
-    int rc = stream_slot(ds, stream, &w);
-    if (rc) return rc;
-    if ((rc = grow(&w->sws, &w->sws_bytes, bytes, stream, ~(size_t)0, "hipMalloc(spec workspace)"))) return rc;
-    if (!w->spec_host) {
-        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-        const bool cap = capturing(stream);
-        if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
-        void* h = nullptr;
-        const hipError_t e = hipHostMalloc(&h, 64, hipHostMallocMapped);
-        if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
-        if (e != hipSuccess) return ws_set_err("hipHostMalloc(spec counter)", e);
-        w->spec_host = reinterpret_cast<u32*>(h);
-        *reinterpret_cast<volatile u32*>(w->spec_host) = ~0u;
-    }
-    *last_repaired = *reinterpret_cast<volatile u32*>(w->spec_host);
-    *out = w->sws;
-    *call = w->spec_calls++;
-    u32* dev_host = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_host), w->spec_host, 0) != hipSuccess) dev_host = nullptr;
-    *host = dev_host;
-    return 0;
-}
-
 // per-call generation number for the piece path's disorder word (never 0)
 u32 ws_next_gen() {
     static std::atomic<u32> s_gen{0};
@@ -325,7 +290,6 @@ int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
 // the decode variant a call takes
 static int decode_path(const WsTuning& t, u64 span, u32 nseg, u32 max_frames) {
     if (t.path == 4) return max_frames <= 64 ? 4 : 3;                 // segfuse holds <= 64 frames per segment
-    if (t.path == 5) return 5;
     if (t.path >= 0) return t.path;
     return ws_segfuse_fits(span, nseg, max_frames) ? 4 : 3;
 }
@@ -354,15 +318,6 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     L.cus = ds->cus;
     u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
     const int path = decode_path(t, hi - lo, nseg, max_frames);
-    if (path == 5) {
-        void* sws = nullptr;
-        u32 call = 0, last = 0;
-        u32* host = nullptr;
-        if ((rc = spec_workspace(ds, ws_spec_workspace_bytes(hi - lo, nseg), L.stream, &sws, &call, &host, &last)))
-            return rc;
-        (void)call;
-        return ws_launch_spec(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(sws), host);
-    }
     if (path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
     if (path == 4) return ws_launch_segfuse(L, t.nt);
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);

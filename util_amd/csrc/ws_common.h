@@ -333,8 +333,6 @@ int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, cons
                     hipStream_t stream, void* ws = nullptr, size_t ws_bytes = 0);
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 int ws_launch_segfuse(const WsLaunch& L, int nt);
-size_t ws_spec_workspace_bytes(u64 span, u32 nseg);
-int ws_launch_spec(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32* host_cnt);
 bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
 
 // Block -> work item with the items split into two windows streamed side by side

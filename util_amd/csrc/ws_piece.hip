@@ -221,7 +221,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     }
 }
 
-template <int NT, u32 WHOLE, int OCC, int PROBE = 0>
+template <int NT, u32 WHOLE, int OCC>
 __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
                                                                   const u64* __restrict__ seg_len, u32 nseg,
@@ -235,7 +235,6 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   u32 wshift, u32 wbit, u64 ppw, u64 npieces, u32 wn) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const u64 lead0_k = reinterpret_cast<uintptr_t>(buf) & 15;
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
@@ -263,35 +262,6 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
         reinterpret_cast<uintptr_t>(ptr + pidx));
     const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
-    // EXPERIMENT (option "k2_probe"): the cost of a self-walk by scalar loads — the segment's
-    // first header, then 15 stride candidates, all through the scalar cache, while the payload
-    // loads are in flight; the result only feeds a never-taken store
-    u32 probe_acc = 0;
-    if constexpr (PROBE) {
-        const u32 ps = (u32)(pv >> 32);
-        if (pvalid && pv != PIECE_NONE && ps < nseg) {
-            typedef __attribute__((address_space(4))) const u64 cu64;
-            const u64 so = *reinterpret_cast<cu64*>(reinterpret_cast<uintptr_t>(seg_off + ps));
-            const uintptr_t sp = reinterpret_cast<uintptr_t>(buf) + so;
-            const cu32* h0p = reinterpret_cast<const cu32*>(sp & ~(uintptr_t)3);
-            const u32 a0 = h0p[0], a1 = h0p[1];
-            const u64 hw = ((u64)a0 | ((u64)a1 << 32)) >> (8 * (sp & 3));
-            const u32 p7 = (u32)(hw >> 8) & 0x7Fu;
-            const u32 plen = p7 < 126 ? p7 : (((u32)(hw >> 16) & 0xFFu) << 8 | ((u32)(hw >> 24) & 0xFFu));
-            const u64 g = 2 + (p7 == 126 ? 2 : 0) + 4 + plen;
-            const u64 pend_b = ((pbase + pidx + 1) << PIECE_SHIFT) - lead0_k;
-            typedef __attribute__((address_space(4))) const u32x4 cu32x4;
-            u32x4 hv[15];
-#pragma unroll
-            for (u32 k = 1; k < 16; ++k) {               // 15 independent loads, then one wait
-                const u64 pos = so + k * g;
-                const uintptr_t q = reinterpret_cast<uintptr_t>(buf) + (pos < pend_b ? pos : so);
-                hv[k - 1] = *reinterpret_cast<cu32x4*>(q & ~(uintptr_t)3);
-            }
-#pragma unroll
-            for (u32 k = 0; k < 15; ++k) probe_acc ^= hv[k].x ^ hv[k].y ^ hv[k].z ^ hv[k].w;
-        }
-    }
     u32 m[PIECE_U][4];
     u32 cov[PIECE_U];
 #pragma unroll
@@ -382,9 +352,6 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
             ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
         }
     }
-    if constexpr (PROBE) {
-        if (probe_acc == 0x9E3779B9u && wshift == 77u) *gptr<u32>(disorder) = probe_acc;   // never: wshift <= 6
-    }
     // K1 found the segments out of buffer order (or outside [lo, hi)): nothing was stored
     // above; the batch is decoded here instead, one wavefront per segment (ws_walk.h)
     if (!ok) {
@@ -463,7 +430,6 @@ WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 
 // K2 launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
 // recorded K2 durations, "k2_calls" counts them; setting the option clears the record.
 WsOpt ws_k2_timing{0};
-WsOpt ws_k2_probe{0};     // EXPERIMENT "k2_probe": K2 with a scalar-load self-walk probe (results unchanged)
 static std::vector<hipEvent_t> g_k2ev;    // start, end, start, end, ...
 static size_t g_k2n = 0;
 static std::mutex g_k2mu;
@@ -515,7 +481,6 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
                                    : (whole == 1 ? ws_piece_unmask_kernel<0, 1, 1> : ws_piece_unmask_kernel<0, 0, 1>));
     if (occ == 7 || occ == 8)                              // forced occupancy: spills, measured slower
         k = occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
-    if (ws_k2_probe) k = ws_piece_unmask_kernel<1, 2, 1, 1>;
     u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
     const u32 wbit = wshift ? (u32)(pwbit < 0 ? 0 : (pwbit > 8 ? 8 : pwbit)) : 0u;

@@ -638,7 +638,6 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return ws_set_err("stream walk records", e);
-    const auto t_rec = std::chrono::steady_clock::now();
     // follow the chain from P: exact, every record is the reference loop from its start
     std::vector<u64> ht;
     u64 ent = P;

@@ -90,44 +90,3 @@ __device__ __forceinline__ void walk_segment(unsigned char* __restrict__ buf, u3
     }
     if (lane == 0) ws_store_res(res + s, off, nf, status);
 }
-
-
-// The same walk with every header read by vector loads that bypass L1 (nontemporal), for a
-// wave that has just rewritten bytes of the segment itself (ws_spec.hip's repair: the undo
-// restores bytes that true headers may occupy; the scalar cache could still hold them as they
-// were). Each header is one round trip behind the previous frame's stores: repair path only.
-template <int U, int NT>
-__device__ __forceinline__ void walk_segment_vload(unsigned char* __restrict__ buf, u32 s,
-                                                   const u64* __restrict__ seg_off, const u64* __restrict__ seg_len,
-                                                   u32 max_frames, const u64* __restrict__ desc_base,
-                                                   WebsocketFrameDesc_t* __restrict__ desc,
-                                                   WebsocketSegResult_t* __restrict__ res, u32 lane) {
-    const u64 so = seg_off[s], sl = seg_len[s];
-    const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
-    unsigned char* const seg = buf + so;
-    u64 off = 0;
-    u32 nf = 0;
-    int status = WEBSOCKET_SEG_OK;
-    while (off < sl) {
-        if (nf >= max_frames) { status = WEBSOCKET_SEG_MAX_FRAMES; break; }
-        const u64 avail = sl - off;
-        if (avail < 2) break;                                           // websocketframe.c:121
-        unsigned char* const p = seg + off;
-        const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
-        const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                // this wave's stores first
-        const u32x4 x0 = __builtin_nontemporal_load(q), x1 = __builtin_nontemporal_load(q + 1);
-        u64 h0, h1;
-        ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
-        const WsHdr h = ws_parse(h0, h1, avail);
-        if (h.kind == WS_PARSE_INCOMPLETE) break;
-        if (h.kind == WS_PARSE_WRAP) { status = WEBSOCKET_SEG_ERR_LEN_WRAP; break; }
-        if (h.masked) unmask_payload<U, NT>(p + h.hdr, p + h.hdr + h.plen, h.key, lane);
-        if (h.ret == 0) break;                                          // (int) truncated to 0
-        if (lane == 0) ws_store_desc(desc + dbase + nf, so + off, h);
-        ++nf;
-        if (h.ret < 0) { status = WEBSOCKET_SEG_ERR_DECODE; break; }    // net_reactor.c:518-520
-        off += (u32)h.ret;                                              // net_reactor.c:525
-    }
-    if (lane == 0) ws_store_res(res + s, off, nf, status);
-}
