@@ -6,9 +6,17 @@
 A step = one websocketframeBatchDecodeDevice call over the whole synthetic batch
 (BASELINE.json configs[1]: 1,048,576 masked binary frames x 4 KiB payload, split
 into rx segments of 16 frames = 65,536 connections), in place, inputs resident
-in HBM. value = payload GiB/s over all ranks (weak scaling: every rank decodes
-its own full batch; frames are independent, no collective in the data path —
-RCCL only carries the max-over-ranks time). Prints ONE JSON line on rank 0.
+in HBM. value = payload GiB/s over all ranks (weak scaling: rank r decodes frames
+[r*n, (r+1)*n) of one seeded stream; frames are independent, no collective in the data
+path — RCCL only carries the max-over-ranks time, counts and the output hash).
+roofline.frac is the step's (the contract's timed region: walk + unmask); the unmask
+kernel alone is reported as roofline.kernel_frac.
+
+--config cfg4: BASELINE configs[3] as STRONG scaling — ONE global batch of 8 M x 64 KiB
+frames (549.9 GB of wire) sharded over the ranks by segment ranges, each rank generating
+its share where it decodes it, in rounds that fit its HBM; a step = one pass over the whole
+batch; the output hash (util_amd/dist.py:run_shard) is the same for every N.
+Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes as C
@@ -109,22 +117,24 @@ class Workload:
     }
 
     @classmethod
-    def make(cls, name, dev, nframes=None, seed_offset=0, fps=None, plen=None):
+    def make(cls, name, dev, nframes=None, fps=None, plen=None, first_frame=0, seed_offset=0):
+        """generator frames first_frame .. first_frame + nframes - 1 of the config's seeded
+        stream (rank r of a weak-scaling run: first_frame = r * nframes)"""
         from util_amd import synth
         n, pk, fl, bk, seed, fps0 = cls.CONFIGS[name]
         fps = fps or fps0
         fl = plen or fl
         if nframes is not None:
             n = nframes
-        return cls(name, dev, n, pk, fl, bk, seed + seed_offset, fps, synth)
+        return cls(name, dev, n, pk, fl, bk, seed + seed_offset, fps, synth, first_frame)
 
-    def __init__(self, name, dev, n, pk, fl, bk, seed, fps, gen):
+    def __init__(self, name, dev, n, pk, fl, bk, seed, fps, gen, first_frame=0):
         import torch
         from util_amd import wsframe as W
         self.torch, self.W = torch, W
         self.name, self.dev, self.nframes, self.plen_kind, self.fixed_len = name, dev, n, pk, fl
-        self.b0_kind, self.seed, self.fps = bk, seed, fps
-        plen = gen.plens(pk, fl, seed, n)
+        self.b0_kind, self.seed, self.fps, self.first_frame = bk, seed, fps, first_frame
+        plen = gen.plens(pk, fl, seed, n, first_frame)
         wl = gen.wirelens(plen)
         off = np.zeros(n, dtype=np.uint64)
         off[1:] = np.cumsum(wl[:-1], dtype=np.uint64)
@@ -143,7 +153,7 @@ class Workload:
         self.desc = t.empty(self.nseg * fps * 32, dtype=t.uint8, device=dev)
         self.res = t.empty(self.nseg * 16, dtype=t.uint8, device=dev)
         self.buf[self.wire_bytes:].zero_()
-        W.synth_device(self.buf, self.frame_off, n, pk, fl, bk, seed)
+        W.synth_device(self.buf, self.frame_off, n, pk, fl, bk, seed, first_frame=first_frame)
         self.decodes = 0
 
     # algorithmic HBM bytes of one decode: read every wire byte, write every payload byte
@@ -159,9 +169,18 @@ class Workload:
         t = self.torch
         mm = t.zeros(1, dtype=t.int64, device=self.dev)
         self.W.synth_verify_device(self.buf, self.frame_off, self.nframes, self.plen_kind, self.fixed_len, self.seed,
-                                   expect_plain, mm)
+                                   expect_plain, mm, first_frame=self.first_frame)
         t.cuda.synchronize()
         return int(mm.item())
+
+    def output_hash(self):
+        """util_amd/dist.py:frame_hash summed over the batch's decoded frames (the buffer as it
+        is now: hash it after an odd number of decodes)"""
+        t = self.torch
+        h = t.zeros(1, dtype=t.int64, device=self.dev)
+        self.W.frame_hash_device(self.buf, self.desc, self.res, self.nseg, self.fps, h)
+        t.cuda.synchronize()
+        return int(h.item()) & 0xFFFFFFFFFFFFFFFF
 
     def check_descs(self):
         """descriptors of every frame equal what websocketframeDecode returns for the generator's frames"""
@@ -178,7 +197,7 @@ class Workload:
         ret = rest[:n] & 0xFFFFFFFF
         assert t.equal(ret, wl)
         flags = (rest[:n] >> 32) & 0xFFFFFFFF
-        f = t.arange(n, device=self.dev)
+        f = t.arange(self.first_frame, self.first_frame + n, device=self.dev)
         if self.b0_kind == 2:
             j = f & 15
             fin = (j == 15).long()
@@ -282,7 +301,7 @@ def run_encode(args, dev, world, rank):
                               "ws_enc_copy_kernel + ws_enc_edge_kernel",
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
-        "cpu_baseline": cpu_encode_baseline(wl, min(args.cpu_threads, os.cpu_count() or 1))
+        "cpu_baseline": cpu_encode_baseline(wl, args.cpu_threads or cpu_thread_counts()[-1])
         if rank == 0 and world == 1 and not args.no_cpu else None,
     }
     if rank == 0:
@@ -353,7 +372,8 @@ def run_stream(args, dev, world, rank):
     import torch
     from util_amd import dist as D
     from util_amd import wsframe as W
-    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank)
+    nfr = args.frames or Workload.CONFIGS[args.config][0]
+    wl = Workload.make(args.config, dev, nframes=args.frames, first_frame=rank * nfr)
     res = torch.zeros(16, dtype=torch.uint8, device=dev)
 
     def step():
@@ -400,7 +420,7 @@ def run_reasm(args, dev, world, rank):
     import torch
     from util_amd import dist as D
     from util_amd import wsframe as W
-    wl = Workload.make(args.config, dev, seed_offset=rank)
+    wl = Workload.make(args.config, dev, first_frame=rank * Workload.CONFIGS[args.config][0])
     out = torch.empty(wl.wire_bytes + 64, dtype=torch.uint8, device=dev)
     msg = torch.empty(wl.nseg * wl.fps * 32, dtype=torch.uint8, device=dev)
     nmsg = torch.empty(wl.nseg, dtype=torch.int32, device=dev)
@@ -436,8 +456,7 @@ def run_reasm(args, dev, world, rank):
     pmc = pmc_traffic(kname, algo)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(wl.host_sample(262144), min(args.cpu_threads, os.cpu_count() or 1), op="reasm",
-                           frames_per_segment=wl.fps)
+        cpu = cpu_baseline(wl.host_sample(262144), args.cpu_threads or None, op="reasm", frames_per_segment=wl.fps)
     out_json = {
         "metric": "WebSocket fused unmask + message reassembly GiB/s of bodies (device-resident)",
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
@@ -498,43 +517,54 @@ def end_to_end(wl, runs=2):
             "path": "websocketframeBatchDecodeHost: H2D | decode | D2H over 64 MiB groups, 3 streams"}, runs + 1
 
 
-def cpu_baseline(sample, threads, min_seconds=1.0, op="decode", frames_per_segment=16):
-    """time the reference's own websocketframeDecode (oracle/_ref, reactor loop driver) —
-    or the oracle restatement when the reference build is absent — on host cores.
-    op "reasm": the same loop delivering messages as the reactor's stream hook does
-    (oracle/ref_loop.c:ref_reassemble_segments: packet cache + merge copies)."""
+def cpu_thread_counts():
+    """(1, the box's CPU share for this job (OMP_NUM_THREADS, 16 on the GPU box), every CPU
+    this process may run on (sched_getaffinity: nproc)), deduplicated, ascending"""
+    allc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or allc
+    return sorted({1, min(share, allc), allc})
+
+
+def cpu_baseline(sample, threads=None, min_seconds=1.0, op="decode", frames_per_segment=16):
+    """Time the reference's own websocketframeDecode (oracle/_ref, compiled from the reference
+    sources, driven by the reactor loop net_reactor.c:515-526: kind "reference") and the
+    oracle restatement (oracle/ws_oracle.c: kind "port") on host cores, on a bounded sample of
+    the workload, at 1 thread, at the job's CPU share and at every CPU of the process
+    (threads=None) — SURVEY §8d. op "reasm": the same loop delivering messages as the reactor's
+    stream hook does (oracle/ref_loop.c:ref_reassemble_segments). `value` is the all-CPU rate."""
     buf, so, sl, payload = sample
     ref = os.path.join(REPO, "oracle", "_ref", "libwsref_loop.so")
     what = "reactor loop net_reactor.c:515-526 over websocketframeDecode"
-    if op == "reasm":
-        if not os.path.exists(ref):
-            return None
-        what += " + fragment cache/merge delivery net_channel_ex.c:55-157 (restated glue)"
+    runners = {}
     if os.path.exists(ref):
         lib = C.CDLL(ref)
         fn = lib.ref_reassemble_segments if op == "reasm" else lib.ref_decode_segments
         fn.restype = C.c_ulonglong
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]
-        kind = "reference" if op == "decode" else "port"
 
-        def run(lo, hi):
+        def run_ref(lo, hi, _fn=fn):
             nf = C.c_ulonglong()
-            fn(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo, C.byref(nf))
-    else:
+            _fn(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo, C.byref(nf))
+        runners["reference" if op == "decode" else "port"] = run_ref
+        if op == "reasm":
+            what += " + fragment cache/merge delivery net_channel_ex.c:55-157 (restated glue)"
+    if op == "decode":
         sys.path.insert(0, os.path.join(REPO, "tests"))
         from oracle_lib import load_oracle
         from util_amd.wsframe import DESC_DTYPE, SEGRES_DTYPE
-        lib = load_oracle()
-        kind = "port"
+        olib = load_oracle()
 
-        def run(lo, hi):
-            d = np.empty((hi - lo) * 16, DESC_DTYPE)
+        def run_port(lo, hi):
+            d = np.empty((hi - lo) * frames_per_segment, DESC_DTYPE)
             r = np.empty(hi - lo, SEGRES_DTYPE)
-            lib.ws_oracle_decode_segments(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo, 16,
-                                          None, d.ctypes.data, r.ctypes.data)
+            olib.ws_oracle_decode_segments(buf.ctypes.data, so[lo:hi].ctypes.data, sl[lo:hi].ctypes.data, hi - lo,
+                                           frames_per_segment, None, d.ctypes.data, r.ctypes.data)
+        runners.setdefault("port", run_port)
+    if not runners:
+        return None
     nseg = len(so)
 
-    def timed(nthreads, passes):
+    def timed(run, nthreads, passes):
         bounds = np.linspace(0, nseg, nthreads + 1).astype(int)
 
         def worker(i):
@@ -548,18 +578,139 @@ def cpu_baseline(sample, threads, min_seconds=1.0, op="decode", frames_per_segme
             th.join()
         return time.perf_counter() - t0
 
-    # calibrate passes so the multi-thread run lasts about min_seconds of wall time
-    t1 = timed(1, 1)
-    single = payload / t1 / 2**30
-    passes = max(2, int(min_seconds / max(1e-6, t1 / threads)))
-    passes += passes % 2  # even: buffer returns to its masked state
-    tn = timed(threads, passes)
-    multi = payload * passes / tn / 2**30
-    return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "single_thread_gibs": round(single, 3),
-            "cpu_seconds": round(tn * threads + t1, 2),
-            "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %d passes x %d threads, "
-                      "%s" % (nseg * frames_per_segment, nseg, payload / 2**20, passes, threads, what)}
+    counts = cpu_thread_counts() if threads is None else sorted({1, threads})
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or counts[-1]
+    rates, wall = {}, 0.0
+    for kind, run in runners.items():
+        t1 = timed(run, 1, 1)
+        wall += t1
+        rates[kind] = {1: payload / t1 / 2**30}
+        for n in counts[1:]:
+            # `passes` whole samples, sized so the run lasts about min_seconds on the CPUs the job
+            # may actually use (the box grants OMP_NUM_THREADS of them, whatever nproc says);
+            # even: the buffer returns to its masked state
+            passes = max(2, int(min_seconds * min(n, share) / max(1e-6, t1)))
+            passes += passes % 2
+            tn = timed(run, n, passes)
+            wall += tn
+            rates[kind][n] = payload * passes / tn / 2**30
+    kind = "reference" if "reference" in rates else "port"
+    top = counts[-1]
+    out = {"value": round(rates[kind][top], 3), "unit": "GiB/s", "cores": top, "kind": kind,
+           "threads": {str(n): round(v, 3) for n, v in rates[kind].items()},
+           "single_thread_gibs": round(rates[kind][1], 3),
+           "cpu_count": os.cpu_count(), "affinity_cpus": counts[-1],
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "wall_seconds": round(wall, 2),
+           "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %s; threads %s"
+                     % (nseg * frames_per_segment, nseg, payload / 2**20, what, counts)}
+    if kind == "reference" and "port" in rates:
+        out["port"] = {"kind": "port", "what": "oracle/ws_oracle.c (the restatement, same flags)",
+                       "threads": {str(n): round(v, 3) for n, v in rates["port"].items()}}
+    return out
+
+
+STRONG = {"cfg4": 8 << 20}     # config -> global frames of its strong-scaling batch (BASELINE configs[3])
+
+
+def run_strong(args, dev, world, rank):
+    """BASELINE configs[3] as strong scaling: ONE global batch (8 M x 64 KiB masked frames,
+    16-frame rx segments, 549.9 GB of wire) split over the ranks by segment ranges
+    (util_amd/dist.py:run_shard); each rank generates its share where it decodes it (frames by
+    global index, websocketframeSynthDeviceRange), in rounds of at most --round-frames frames
+    (1 M = 68.7 GB of wire by default: 8 rounds on one GPU, one on each of 8). Per round:
+    generate, `warmup` decodes, `steps` decodes timed with HIP events at the region's two ends,
+    one more if needed so the buffer holds plaintext, the output hash, the generator check.
+    A step = one pass over the whole batch: ms_per_step = max over ranks of the sum over its
+    rounds of the per-call decode time; value = the batch's payload / that."""
+    import torch
+    from util_amd import dist as D
+    from util_amd import synth
+    from util_amd import wsframe as W
+    n_total = args.global_frames or STRONG[args.config]
+    n, pk, fl, bk, seed, fps = Workload.CONFIGS[args.config]
+    assert pk == 0, "strong mode: fixed-size frames"
+    nseg_total = n_total // fps
+    per_round = max(1, (args.round_frames or (1 << 20)) // fps)
+    first_seg, count = D.segment_shard(nseg_total, world, rank)
+    max_segs = min(per_round, count) if count else 1
+    wirelen = int(synth.wirelens(np.array([fl], np.uint64))[0])
+    cap = max_segs * fps * wirelen
+    buf = torch.empty(cap + 256, dtype=torch.uint8, device=dev)
+    buf[cap:].zero_()
+    desc = torch.empty(max_segs * fps * 32, dtype=torch.uint8, device=dev)
+    res = torch.empty(max_segs * 16, dtype=torch.uint8, device=dev)
+    hsh = torch.zeros(1, dtype=torch.int64, device=dev)
+    mm = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def decode_round(s, nseg):
+        nf = nseg * fps
+        foff = torch.arange(nf, dtype=torch.int64, device=dev) * wirelen
+        so = foff[::fps].contiguous()
+        sl = torch.full((nseg,), fps * wirelen, dtype=torch.int64, device=dev)
+        b = buf[:nf * wirelen + 256]
+        W.synth_device(b, foff, nf, pk, fl, bk, seed, first_frame=s * fps)
+
+        def call():
+            W.batch_decode_device(b, so, sl, fps, desc, res)
+        for _ in range(args.warmup):
+            call()
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(args.steps):
+            call()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / max(1, args.steps)
+        if (args.warmup + args.steps) % 2 == 0:
+            call()                                                # odd: the buffer holds plaintext
+        hsh.zero_()
+        mm.zero_()
+        W.frame_hash_device(b, desc, res, nseg, fps, hsh)
+        W.synth_verify_device(b, foff, nf, pk, fl, seed, True, mm, first_frame=s * fps)
+        r = res[:nseg * 16].view(torch.int64).view(-1, 2)
+        frames = int((r[:, 1] & 0xFFFFFFFF).sum())
+        bad_status = int(((r[:, 1] >> 32) != 0).sum()) + int(int(r[:, 0].sum()) != nf * wirelen)
+        torch.cuda.synchronize()
+        return dict(frames=frames, payload=nf * fl, wire=nf * wirelen, errors=int(mm.item()) + bad_status,
+                    hash=int(hsh.item()) & 0xFFFFFFFFFFFFFFFF, seconds=ms / 1e3)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    t0 = time.perf_counter()
+    loc, glob = D.run_shard(nseg_total, world, rank, per_round, decode_round, device=dev)
+    wall = D.allreduce([time.perf_counter() - t0], op="max", device=dev)[0]
+    step_s = glob["seconds"]
+    algo = glob["wire"] + glob["payload"]
+    out = {
+        "metric": "WebSocket unmask GiB/s (device-resident), 8M x 64KiB frames sharded across GPUs",
+        "value": round(glob["payload"] / step_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, each shard generated in HBM "
+                "by global frame index)",
+        "config": {"workload": "8M masked binary frames x 64 KiB, 16-frame rx segments, one batch sharded by segment "
+                               "ranges", "config": args.config, "global_frames": n_total,
+                   "global_wire_bytes": glob["wire"], "global_payload_bytes": glob["payload"],
+                   "rounds_per_rank": loc["rounds"], "frames_per_round": per_round * fps,
+                   "parallelism": "segment-range shards over %d GPU(s), no data-path collective" % world},
+        "roofline": {"bound": "hbm", "achieved": round(algo / world / step_s / 1e9, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s per GPU", "frac": round(algo / world / step_s / 1e9 / PEAK_HBM_GBS, 4),
+                     "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_step": algo,
+                     "timed": "per round: HIP events at the two ends of `steps` back-to-back decode calls; step = "
+                              "sum over the rank's rounds, max over ranks (generation, hashing and checks between "
+                              "rounds are outside)"},
+        "verified": glob["errors"] == 0 and glob["frames"] == n_total,
+        "output_hash": "%016x" % glob["hash"],
+        "allreduced": {"frames": glob["frames"], "payload_bytes": glob["payload"], "errors": glob["errors"]},
+        "wall_s_incl_generation": round(wall, 2),
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    return 0 if out["verified"] else 1
 
 
 def run_inflight(args, wl0, dev, world, rank):
@@ -573,8 +724,8 @@ def run_inflight(args, wl0, dev, world, rank):
     import torch
     import torch.distributed as dist
     k = args.inflight
-    wls = [wl0] + [Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank + 7919 * i, fps=args.fps,
-                                 plen=args.plen) for i in range(1, k)]
+    wls = [wl0] + [Workload.make(args.config, dev, nframes=args.frames, fps=args.fps, plen=args.plen,
+                                 first_frame=wl0.first_frame, seed_offset=7919 * i) for i in range(1, k)]
     streams = [torch.cuda.Stream(dev) for _ in range(k)]
     base = torch.cuda.current_stream()
     base.synchronize()
@@ -623,7 +774,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: 1, the job's share (OMP_NUM_THREADS) and every CPU of the process)")
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
     ap.add_argument("--graph", action="store_true",
@@ -634,6 +786,10 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="override the config's frame count (experiments)")
     ap.add_argument("--fps", type=int, default=None, help="override frames per rx segment (experiments)")
     ap.add_argument("--plen", type=int, default=None, help="override the fixed payload length (experiments)")
+    ap.add_argument("--global-frames", type=int, default=None,
+                    help="strong-scaling configs (cfg4): frames of the global batch (default 8M)")
+    ap.add_argument("--round-frames", type=int, default=None,
+                    help="strong-scaling configs: frames per round on one GPU (default 1M = 68.7 GB of wire)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="decode: also time K independent batches of the config in flight together, one HIP "
                          "stream each (a reactor with successive rx batches), reported as the 'inflight' field "
@@ -665,14 +821,15 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     dev = torch.device("cuda", gpu)
-    if args.op in ("encode", "reasm", "stream"):
-        mism = {"encode": run_encode, "reasm": run_reasm, "stream": run_stream}[args.op](args, dev, world, rank)
+    if args.op in ("encode", "reasm", "stream") or (args.op == "decode" and args.config in STRONG):
+        fn = {"encode": run_encode, "reasm": run_reasm, "stream": run_stream, "decode": run_strong}[args.op]
+        mism = fn(args, dev, world, rank)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)
 
-    wl = Workload.make(args.config, dev, nframes=args.frames, seed_offset=rank, fps=args.fps,
-                       plen=args.plen)
+    nfr = args.frames or Workload.CONFIGS[args.config][0]
+    wl = Workload.make(args.config, dev, nframes=args.frames, fps=args.fps, plen=args.plen, first_frame=rank * nfr)
     torch.cuda.synchronize()
     sample = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -725,19 +882,26 @@ def main():
     if args.inflight > 1:
         inflight, m = run_inflight(args, wl, dev, world, rank)
         mism += m
-    mism = int(D.allreduce([mism], device=dev)[0])
+    # the output hash of the decoded batch (plaintext state), summed over ranks: the global
+    # stream's frames [0, world * n) (util_amd/dist.py:frame_hash)
+    if wl.decodes % 2 == 0:
+        wl.decode()
+    h = wl.output_hash()
+    mism += wl.verify(expect_plain=True)
+    mism, = D.allreduce([mism], device=dev)
+    mism = int(mism)
+    ghash = D.allreduce_u64([h], device=dev)[0]
 
     payload_all = wl.payload_bytes * world * args.steps
     value = payload_all / elapsed / 2**30
     step_kern = float(kern_ms.mean()) / 1e3
     mean_kern = k2_ms / 1e3 if k2_ms else step_kern
-    achieved = wl.algo_bytes / mean_kern / 1e9
+    achieved = wl.algo_bytes / step_kern / 1e9                      # the step: the contract's timed region
     pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes)
-    timed = ("HIP events recorded around every ws_piece_unmask_kernel launch on the calls' stream "
-             "(library option k2_timing), %d calls; step (K1 + K2) from the contract's region: %.4f ms = %.4f of peak"
-             % (args.steps, step_kern * 1e3, wl.algo_bytes / step_kern / 1e9 / PEAK_HBM_GBS)) if k2_ms else \
-        ("HIP events at the two ends of the timed region on the calls' stream / steps: " +
-         STEP_KERNELS.get(kpath, KERNELS[kpath]))
+    timed = ("HIP events at the two ends of the contract's timed region on the calls' stream / steps: " +
+             STEP_KERNELS.get(kpath, KERNELS[kpath]))
+    kernel_timed = ("HIP events recorded around every ws_piece_unmask_kernel launch on the calls' stream (library "
+                    "option k2_timing), a second region of %d calls" % args.steps) if k2_ms else timed
     out = {
         "metric": "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames",
         "value": round(value, 2),
@@ -759,19 +923,23 @@ def main():
                      "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
                      "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
+                     "traffic_kernels": pmc[1].get("kernels_summed") if pmc else None,
                      "kernel": KERNELS[kpath], "algo_bytes_per_launch": wl.algo_bytes,
                      "timed": timed,
-                     "per_kernel_ns_profiled": pmc[1].get("per_kernel_avg_ns") if pmc else None,
+                     "step_ms_mean": round(step_kern * 1e3, 4),
                      "kernel_ms_mean": round(mean_kern * 1e3, 4),
-                     "step_ms_mean": round(step_kern * 1e3, 4)},
+                     "kernel_frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
+                     "kernel_timed": kernel_timed,
+                     "per_kernel_ns_profiled": pmc[1].get("per_kernel_avg_ns") if pmc else None},
         "verified": mism == 0,
+        "output_hash": "%016x" % ghash,
         "cpu_baseline": None,
         "e2e": e2e,
     }
     if inflight is not None:
         out["inflight"] = inflight
     if sample is not None:
-        out["cpu_baseline"] = cpu_baseline(sample, min(args.cpu_threads, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(sample, args.cpu_threads or None)
     if args.scatter and world > 1:                                 # SURVEY §8e (1), outside the timed region
         recv = None if rank == 0 else torch.empty(wl.wire_bytes, dtype=torch.uint8, device=dev)
         dt = D.allreduce([D.scatter_from_root(wl.buf, recv, wl.wire_bytes)], op="max", device=dev)[0]

@@ -4,6 +4,7 @@ reference's golden vectors. Bit-exact: buffer bytes, descriptors, segment result
 Full-size configs are checked by size-independent properties (decode restores
 the generator's plaintext; decoding twice restores the wire bytes)."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -208,10 +209,11 @@ def test_synth_matches_numpy_generator(dev):
         assert np.array_equal(d.cpu().numpy(), wire)
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
 def test_full_size_properties(dev, cfg):
-    """BASELINE configs at full size: decode -> generator plaintext; decode again -> wire bytes;
-    descriptors/segment results consistent with the generator's lengths"""
+    """BASELINE configs at full size (cfg4: one GPU's share of the 8-GPU batch, 1 M x 64 KiB =
+    68.7 GB of wire in 16-frame rx segments): decode -> generator plaintext; decode again ->
+    wire bytes; descriptors/segment results consistent with the generator's lengths"""
     import bench
     wl = bench.Workload.make(cfg, dev)
     try:
@@ -342,3 +344,60 @@ def test_window_mappings(dev, decode_path, opt, val):
     finally:
         W.set_option("piece_win", 1)
         W.set_option("seg_win", 1)
+
+
+def test_cfg4_shape_vs_oracle(dev, decode_path):
+    """cfg4's layout (64 KiB masked frames, 16-frame rx segments, 64-bit length form) at reduced
+    size, bit-exact vs the oracle: generator frames taken from the middle of the global batch
+    (a rank's shard)"""
+    if decode_path == 4:
+        pytest.skip("segfuse is chosen only for segments <= 17 KiB")
+    wire, off, pl, plain = wsynth.make_batch(64, wsynth.PLEN_FIXED, 65536, wsynth.B0_BINARY, 4, first=5 << 20)
+    so = [int(off[i]) for i in range(0, 64, 16)]
+    ends = so[1:] + [len(wire)]
+    gb, gd, gr = assert_same(dev, wire, so, [e - a for a, e in zip(so, ends)], 16, tag="cfg4 shape")
+    assert np.array_equal(gb, plain)
+
+
+def test_output_hash_matches_numpy(dev, decode_path):
+    """websocketframeFrameHashDevice (the multi-GPU output hash) equals its numpy statement
+    util_amd/dist.py:batch_hash on a random batch (every length form, empty and unmasked frames)"""
+    from util_amd import dist as D
+    if decode_path != -1:
+        pytest.skip("one decode path is enough")
+    rng = np.random.default_rng(17)
+    wire, so, sl = random_stream(rng, 400)
+    gb, gd, gr = gpu_decode(dev, wire.copy(), so, sl, 16)
+    h_np = D.batch_hash(gb, gd, gr, 16)
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    d[:n] = torch.from_numpy(gb).to(dev)
+    desc = torch.from_numpy(gd.view(np.uint8).copy()).to(dev)
+    res = torch.from_numpy(gr.view(np.uint8).copy()).to(dev)
+    h = torch.zeros(1, dtype=torch.int64, device=dev)
+    W.frame_hash_device(d, desc, res, len(so), 16, h)
+    torch.cuda.synchronize()
+    assert (int(h.item()) & 0xFFFFFFFFFFFFFFFF) == h_np and h_np != 0
+
+
+def test_strong_scaling_hash_independent_of_rounds(decode_path):
+    """bench.py --config cfg4 (one global batch sharded over ranks, rounds per rank): the
+    output hash, frame count and verification do not depend on the round size (reduced batch:
+    65,536 x 64 KiB frames = 4.3 GB, one round vs four)"""
+    import json
+    import subprocess
+    import sys
+    if decode_path != -1:
+        pytest.skip("runs the default path in a subprocess")
+    outs = []
+    for rf in (65536, 16384):
+        p = subprocess.run([sys.executable, "bench.py", "--config", "cfg4", "--global-frames", "65536",
+                            "--round-frames", str(rf), "--steps", "2", "--warmup", "1"],
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        outs.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    assert all(o["verified"] for o in outs)
+    assert outs[0]["output_hash"] == outs[1]["output_hash"]
+    assert outs[0]["allreduced"]["frames"] == outs[1]["allreduced"]["frames"] == 65536
+    assert outs[1]["config"]["rounds_per_rank"] == 4

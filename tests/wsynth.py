@@ -46,10 +46,11 @@ def header(b0, plen, key):
     return np.array(h, dtype=np.uint8)
 
 
-def make_batch(nframes, plen_kind=PLEN_FIXED, fixed_len=4096, b0_kind=B0_BINARY, seed=1):
+def make_batch(nframes, plen_kind=PLEN_FIXED, fixed_len=4096, b0_kind=B0_BINARY, seed=1, first=0):
     """returns (wire bytes uint8, frame_off uint64, plen uint64, plain bytes concatenated
-    in wire layout, i.e. the expected buffer after one decode)"""
-    pl = plens(plen_kind, fixed_len, seed, nframes)
+    in wire layout, i.e. the expected buffer after one decode) of generator frames
+    first .. first + nframes - 1"""
+    pl = plens(plen_kind, fixed_len, seed, nframes, first)
     wl = wirelens(pl)
     off = np.zeros(nframes, dtype=np.uint64)
     if nframes > 1:
@@ -57,13 +58,13 @@ def make_batch(nframes, plen_kind=PLEN_FIXED, fixed_len=4096, b0_kind=B0_BINARY,
     total = int(wl.sum()) if nframes else 0
     wire = np.empty(total, dtype=np.uint8)
     plain = np.empty(total, dtype=np.uint8)
-    ks = keys(seed, np.arange(nframes, dtype=np.uint64))
-    b0 = b0s(b0_kind, nframes)
+    ks = keys(seed, np.arange(first, first + nframes, dtype=np.uint64))
+    b0 = b0s(b0_kind, first + nframes)[first:]
     for f in range(nframes):
         h = header(b0[f], pl[f], ks[f])
         o = int(off[f])
         hl = len(h)
-        p = plain_payload(seed, f, pl[f])
+        p = plain_payload(seed, first + f, pl[f])
         kb = np.frombuffer(int(ks[f]).to_bytes(4, "little"), dtype=np.uint8)
         m = p ^ np.resize(kb, len(p)) if len(p) else p
         wire[o:o + hl] = h

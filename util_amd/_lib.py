@@ -43,7 +43,8 @@ EXPORTS = REFERENCE_EXPORTS + [
 ]
 # include/wsframe_amd_bench.h (libwsframe_amd_bench.so)
 BENCH_EXPORTS = ["websocketframeSynthDevice", "websocketframeSynthVerifyDevice", "websocketframeGpuCalibrate",
-                 "websocketframeBenchLastError"]
+                 "websocketframeBenchLastError", "websocketframeSynthDeviceRange",
+                 "websocketframeSynthVerifyDeviceRange", "websocketframeFrameHashDevice"]
 
 
 def build_lib(force=False):
@@ -137,6 +138,12 @@ def load_bench_lib():
     lib.websocketframeSynthDevice.argtypes = [vp, vp, u64, i32, u64, i32, u64, vp]
     lib.websocketframeSynthVerifyDevice.restype = i32
     lib.websocketframeSynthVerifyDevice.argtypes = [vp, vp, u64, i32, u64, u64, i32, vp, vp]
+    lib.websocketframeSynthDeviceRange.restype = i32
+    lib.websocketframeSynthDeviceRange.argtypes = [vp, vp, u64, u64, i32, u64, i32, u64, vp]
+    lib.websocketframeSynthVerifyDeviceRange.restype = i32
+    lib.websocketframeSynthVerifyDeviceRange.argtypes = [vp, vp, u64, u64, i32, u64, u64, i32, vp, vp]
+    lib.websocketframeFrameHashDevice.restype = i32
+    lib.websocketframeFrameHashDevice.argtypes = [vp, vp, vp, C.c_uint, C.c_uint, vp, vp]
     lib.websocketframeBenchLastError.restype = C.c_char_p
     lib.websocketframeBenchLastError.argtypes = []
     _bench = lib

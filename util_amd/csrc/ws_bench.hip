@@ -22,13 +22,15 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeBenchLastError(void) { r
 // ---------------------------------------------------------------------------------------------
 // synthetic batches (bench/test input; ws_synth.h)
 
+// frames first + i (global generator indices) at buf + frame_off[i], i < nframes
 __global__ __launch_bounds__(256) void ws_synth_kernel(unsigned char* __restrict__ buf, const u64* __restrict__ frame_off,
-                                                       u64 nframes, int plen_kind, u64 fixed_len, int b0_kind,
+                                                       u64 first, u64 nframes, int plen_kind, u64 fixed_len, int b0_kind,
                                                        u64 seed) {
-    for (u64 f = blockIdx.x; f < nframes; f += gridDim.x) {
+    for (u64 i = blockIdx.x; i < nframes; i += gridDim.x) {
+        const u64 f = first + i;
         const u64 plen = ws_synth_plen(plen_kind, fixed_len, seed, f);
         const u32 key = ws_synth_key(seed, f);
-        unsigned char* p = buf + frame_off[f];
+        unsigned char* p = buf + frame_off[i];
         const u32 hl = ws_synth_headlen(plen) + 4u;
         if (threadIdx.x == 0) {
             unsigned char h[14];
@@ -47,14 +49,15 @@ __global__ __launch_bounds__(256) void ws_synth_kernel(unsigned char* __restrict
 }
 
 __global__ __launch_bounds__(256) void ws_verify_kernel(const unsigned char* __restrict__ buf,
-                                                        const u64* __restrict__ frame_off, u64 nframes, int plen_kind,
-                                                        u64 fixed_len, u64 seed, int expect_plain,
+                                                        const u64* __restrict__ frame_off, u64 first, u64 nframes,
+                                                        int plen_kind, u64 fixed_len, u64 seed, int expect_plain,
                                                         unsigned long long* __restrict__ mismatch) {
     u64 bad = 0;
-    for (u64 f = blockIdx.x; f < nframes; f += gridDim.x) {
+    for (u64 i = blockIdx.x; i < nframes; i += gridDim.x) {
+        const u64 f = first + i;
         const u64 plen = ws_synth_plen(plen_kind, fixed_len, seed, f);
         const u32 key = ws_synth_key(seed, f);
-        const unsigned char* pl = buf + frame_off[f] + ws_synth_headlen(plen) + 4u;
+        const unsigned char* pl = buf + frame_off[i] + ws_synth_headlen(plen) + 4u;
         const u64 km = expect_plain ? 0ULL : ((u64)key | ((u64)key << 32));
         const u64 nw = (plen + 7) >> 3;
         for (u64 j = threadIdx.x; j < nw; j += blockDim.x) {
@@ -67,16 +70,42 @@ __global__ __launch_bounds__(256) void ws_verify_kernel(const unsigned char* __r
     if ((threadIdx.x & 63) == 0 && bad) atomicAdd(mismatch, bad);
 }
 
+extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthDeviceRange(unsigned char* d_buf, const u64* d_frame_off,
+                                                                 unsigned long long first_frame,
+                                                                 unsigned long long nframes, int plen_kind,
+                                                                 unsigned long long fixed_len, int b0_kind,
+                                                                 unsigned long long seed, void* hip_stream) {
+    if (!nframes) return 0;
+    const u32 blocks = nframes < 65536 ? (u32)nframes : 65536u;
+    hipLaunchKernelGGL(ws_synth_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
+                       d_frame_off, (u64)first_frame, (u64)nframes, plen_kind, (u64)fixed_len, b0_kind, (u64)seed);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : ws_set_err("ws_synth_kernel launch", e);
+}
+
 extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthDevice(unsigned char* d_buf, const u64* d_frame_off,
                                                             unsigned long long nframes, int plen_kind,
                                                             unsigned long long fixed_len, int b0_kind,
                                                             unsigned long long seed, void* hip_stream) {
+    return websocketframeSynthDeviceRange(d_buf, d_frame_off, 0, nframes, plen_kind, fixed_len, b0_kind, seed,
+                                          hip_stream);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDeviceRange(const unsigned char* d_buf,
+                                                                       const u64* d_frame_off,
+                                                                       unsigned long long first_frame,
+                                                                       unsigned long long nframes, int plen_kind,
+                                                                       unsigned long long fixed_len,
+                                                                       unsigned long long seed, int expect_plain,
+                                                                       unsigned long long* d_mismatch,
+                                                                       void* hip_stream) {
     if (!nframes) return 0;
     const u32 blocks = nframes < 65536 ? (u32)nframes : 65536u;
-    hipLaunchKernelGGL(ws_synth_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
-                       d_frame_off, (u64)nframes, plen_kind, (u64)fixed_len, b0_kind, (u64)seed);
+    hipLaunchKernelGGL(ws_verify_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
+                       d_frame_off, (u64)first_frame, (u64)nframes, plen_kind, (u64)fixed_len, (u64)seed, expect_plain,
+                       d_mismatch);
     hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : ws_set_err("ws_synth_kernel launch", e);
+    return e == hipSuccess ? 0 : ws_set_err("ws_verify_kernel launch", e);
 }
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned char* d_buf, const u64* d_frame_off,
@@ -84,12 +113,55 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeSynthVerifyDevice(const unsigned
                                                                   unsigned long long fixed_len,
                                                                   unsigned long long seed, int expect_plain,
                                                                   unsigned long long* d_mismatch, void* hip_stream) {
-    if (!nframes) return 0;
-    const u32 blocks = nframes < 65536 ? (u32)nframes : 65536u;
-    hipLaunchKernelGGL(ws_verify_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
-                       d_frame_off, (u64)nframes, plen_kind, (u64)fixed_len, (u64)seed, expect_plain, d_mismatch);
+    return websocketframeSynthVerifyDeviceRange(d_buf, d_frame_off, 0, nframes, plen_kind, fixed_len, seed,
+                                                expect_plain, d_mismatch, hip_stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// output hash of a decoded batch (multi-GPU bit-exactness across shardings): for every
+// descriptor of every segment, ws_frame_hash(datalen, is_fin, type, payload bytes); summed
+// mod 2^64 (order-independent, so any split of the frames over ranks and rounds gives the same
+// total). util_amd/dist.py:frame_hash is the numpy statement of the same function.
+__device__ __forceinline__ u64 ws_frame_hash_word(u64 w, u64 j) { return ws_mix64(w + 0x9E3779B97F4A7C15ULL * (j + 1)); }
+
+__global__ __launch_bounds__(256) void ws_hash_kernel(const unsigned char* __restrict__ buf,
+                                                      const WebsocketFrameDesc_t* __restrict__ desc,
+                                                      const WebsocketSegResult_t* __restrict__ res, u32 nseg,
+                                                      u32 max_frames, unsigned long long* __restrict__ out) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 w = (u64)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (u64)gridDim.x * 4;
+    u64 acc = 0;
+    for (u64 slot = w; slot < (u64)nseg * max_frames; slot += nw) {
+        const u32 s = (u32)(slot / max_frames), k = (u32)(slot % max_frames);
+        if (k >= res[s].n_frames) continue;
+        const WebsocketFrameDesc_t d = desc[slot];
+        const u64 n = d.datalen;
+        const unsigned char* p = d.data_off == WEBSOCKET_DATA_OFF_NULL ? buf : buf + d.data_off;
+        u64 sum = 0;
+        for (u64 j = lane; j < (n + 7) / 8; j += 64) {
+            u64 x = 0;
+            const u64 nb = n - 8 * j < 8 ? n - 8 * j : 8;
+            for (u64 b = 0; b < nb; ++b) x |= (u64)p[8 * j + b] << (8 * b);
+            sum += ws_frame_hash_word(x, j);
+        }
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o);
+        if (lane == 0) acc += ws_mix64(sum ^ n ^ ((u64)d.is_fin << 56) ^ ((u64)d.type << 48));
+    }
+    if (lane == 0 && acc) atomicAdd(out, acc);
+}
+
+extern "C" WSFRAME_AMD_EXPORT int websocketframeFrameHashDevice(const unsigned char* d_buf,
+                                                                const WebsocketFrameDesc_t* d_desc,
+                                                                const WebsocketSegResult_t* d_res, unsigned int nseg,
+                                                                unsigned int max_frames, unsigned long long* d_hash,
+                                                                void* hip_stream) {
+    if (!nseg) return 0;
+    const u64 waves = (u64)nseg * max_frames;
+    const u32 blocks = (u32)(waves / 4 + 1 < 65536 ? waves / 4 + 1 : 65536);
+    hipLaunchKernelGGL(ws_hash_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(hip_stream), d_buf,
+                       d_desc, d_res, nseg, max_frames, d_hash);
     hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : ws_set_err("ws_verify_kernel launch", e);
+    return e == hipSuccess ? 0 : ws_set_err("ws_hash_kernel launch", e);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -2,11 +2,22 @@
 
 Frames are independent, so a batch shards into contiguous segment
 ranges with no data-path collective. The only cross-rank traffic is a handful of
-scalars: the max step time (bench contract) and verification counts — plus, as an
-optional model of a NIC-attached rx buffer on one GPU, `scatter_from_root` (reported
-separately from the decode, never inside its timed region).
+scalars: the max step time (bench contract), verification counts and the output hash
+({frames, payload bytes, errors, output hash}) — plus, as an optional model
+of a NIC-attached rx buffer on one GPU, `scatter_from_root` (reported separately from the
+decode, never inside its timed region).
+
+Strong scaling over one global batch (`run_shard`): rank r decodes segments
+[first, first + count) of ONE seeded batch (generated where it is decoded, by global frame
+index), in rounds when its share exceeds the HBM budget; the per-frame output hash is
+summed mod 2^64, so the all-reduced hash is the same for every world size and round size.
 """
 import numpy as np
+
+from .synth import mix64
+
+U64 = np.uint64
+HASH_C = U64(0x9E3779B97F4A7C15)
 
 
 def byte_balanced_cuts(seg_len, world):
@@ -80,3 +91,86 @@ def scatter_from_root(send, recv, nbytes, root=0):
     dt = time.perf_counter() - t0
     dist.barrier()
     return dt
+
+
+def segment_shard(nseg_total, world, rank):
+    """contiguous, balanced segment range [first, first+count) of `rank` (equal-size
+    segments: balanced by bytes too)"""
+    return frame_shard(nseg_total, world, rank)
+
+
+def shard_rounds(first, count, max_per_round):
+    """[(first_segment, nseg), ...] covering [first, first + count) in rounds of at most
+    max_per_round segments (the shard's HBM budget)"""
+    out, s = [], first
+    while s < first + count:
+        n = min(max_per_round, first + count - s)
+        out.append((s, n))
+        s += n
+    return out
+
+
+def frame_hash(payload, datalen, is_fin, type_):
+    """the output hash of one decoded frame (numpy statement of ws_hash_kernel,
+    util_amd/csrc/ws_bench.hip): mix64(sum_j mix64(w_j + C*(j+1)) ^ datalen ^ fin<<56 ^
+    type<<48) over the payload's little-endian 8-byte words (zero-padded)"""
+    n = int(datalen)
+    b = np.zeros((n + 7) // 8 * 8, np.uint8)
+    b[:n] = np.asarray(payload, dtype=np.uint8)[:n]
+    w = b.view("<u8").astype(np.uint64)
+    j = np.arange(len(w), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        s = mix64(w + HASH_C * (j + U64(1))).sum(dtype=np.uint64) if len(w) else U64(0)
+        return int(mix64(U64(s) ^ U64(n) ^ (U64(int(is_fin)) << U64(56)) ^ (U64(int(type_)) << U64(48))))
+
+
+def batch_hash(buf, desc, res, max_frames):
+    """sum (mod 2^64) of frame_hash over the used descriptors of a decoded batch"""
+    h = 0
+    for s in range(len(res)):
+        for k in range(int(res[s]["n_frames"])):
+            d = desc[s * max_frames + k]
+            n = int(d["datalen"])
+            a = int(d["data_off"]) if n else 0
+            h = (h + frame_hash(buf[a:a + n], n, d["is_fin"], d["type"])) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def allreduce_u64(values, device=None):
+    """exact all-reduce SUM of unsigned 64-bit values mod 2^64 (split into 16-bit limbs so
+    that no limb overflows an int64 sum for any world size)"""
+    import torch
+    import torch.distributed as dist
+    vals = [int(v) & 0xFFFFFFFFFFFFFFFF for v in values]
+    if not (dist.is_available() and dist.is_initialized()):
+        return vals
+    if dist.get_backend() == "gloo":
+        device = None
+    limbs = [(v >> (16 * i)) & 0xFFFF for v in vals for i in range(4)]
+    t = torch.tensor(limbs, dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t = t.tolist()
+    return [sum(int(t[4 * k + i]) << (16 * i) for i in range(4)) & 0xFFFFFFFFFFFFFFFF for k in range(len(vals))]
+
+
+def run_shard(nseg_total, world, rank, max_seg_per_round, decode_round, device=None):
+    """Decode this rank's share of one global batch of nseg_total segments, round by round.
+    decode_round(first_segment, nseg) -> dict(frames, payload, wire, errors, hash, seconds)
+    decodes segments [first, first + nseg) (global indices; it generates them where it
+    decodes them) and returns its counts, its output hash and its timed decode seconds.
+    Returns (local totals, global totals: sums over ranks, seconds = max over ranks)."""
+    first, count = segment_shard(nseg_total, world, rank)
+    loc = dict(frames=0, payload=0, wire=0, errors=0, hash=0, seconds=0.0, rounds=0, segments=count,
+               first_segment=first)
+    for s, n in shard_rounds(first, count, max_seg_per_round):
+        r = decode_round(s, n)
+        for k in ("frames", "payload", "wire", "errors"):
+            loc[k] += int(r[k])
+        loc["hash"] = (loc["hash"] + int(r["hash"])) & 0xFFFFFFFFFFFFFFFF
+        loc["seconds"] += float(r["seconds"])
+        loc["rounds"] += 1
+    frames, payload, wire, errors, h = allreduce_u64([loc["frames"], loc["payload"], loc["wire"], loc["errors"],
+                                                      loc["hash"]], device=device)
+    secs = allreduce([loc["seconds"]], op="max", device=device)[0]
+    glob = dict(frames=frames, payload=payload, wire=wire, errors=errors, hash=h, seconds=secs)
+    return loc, glob

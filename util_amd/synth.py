@@ -23,8 +23,9 @@ def fseed(seed, f):
         return mix64(U64(seed) ^ (f * U64(0xD1B54A32D192ED03)))
 
 
-def plens(plen_kind, fixed_len, seed, n):
-    f = np.arange(n, dtype=np.uint64)
+def plens(plen_kind, fixed_len, seed, n, first=0):
+    """payload lengths of generator frames first .. first + n - 1"""
+    f = np.arange(first, first + n, dtype=np.uint64)
     if plen_kind == PLEN_MIX3:
         r = mix64(fseed(seed, f) ^ U64(0x4C454E)) % U64(3)
         return np.choose(r.astype(np.int64), [125, 1500, 65536]).astype(np.uint64)

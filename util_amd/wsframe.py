@@ -206,18 +206,28 @@ def batch_decode_host(buf, seg_off, seg_len, max_frames, device=0):
     return desc, res[:nseg]
 
 
-def synth_device(buf, frame_off, nframes, plen_kind, fixed_len, b0_kind, seed, stream=None):
-    """websocketframeSynthDevice (libwsframe_amd_bench.so): bench/test input, generated in HBM"""
-    rc = load_bench_lib().websocketframeSynthDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len, b0_kind,
-                                                    seed, _stream(stream))
-    check_bench(rc, "websocketframeSynthDevice")
+def synth_device(buf, frame_off, nframes, plen_kind, fixed_len, b0_kind, seed, stream=None, first_frame=0):
+    """websocketframeSynthDeviceRange (libwsframe_amd_bench.so): bench/test input generated in
+    HBM — generator frames first_frame .. first_frame + nframes - 1 at buf + frame_off[i]"""
+    rc = load_bench_lib().websocketframeSynthDeviceRange(_ptr(buf), _ptr(frame_off), first_frame, nframes, plen_kind,
+                                                         fixed_len, b0_kind, seed, _stream(stream))
+    check_bench(rc, "websocketframeSynthDeviceRange")
 
 
-def synth_verify_device(buf, frame_off, nframes, plen_kind, fixed_len, seed, expect_plain, mismatch, stream=None):
-    rc = load_bench_lib().websocketframeSynthVerifyDevice(_ptr(buf), _ptr(frame_off), nframes, plen_kind, fixed_len,
-                                                          seed, 1 if expect_plain else 0, _ptr(mismatch),
-                                                          _stream(stream))
-    check_bench(rc, "websocketframeSynthVerifyDevice")
+def synth_verify_device(buf, frame_off, nframes, plen_kind, fixed_len, seed, expect_plain, mismatch, stream=None,
+                        first_frame=0):
+    rc = load_bench_lib().websocketframeSynthVerifyDeviceRange(_ptr(buf), _ptr(frame_off), first_frame, nframes,
+                                                               plen_kind, fixed_len, seed, 1 if expect_plain else 0,
+                                                               _ptr(mismatch), _stream(stream))
+    check_bench(rc, "websocketframeSynthVerifyDeviceRange")
+
+
+def frame_hash_device(buf, desc, res, nseg, max_frames, out, stream=None):
+    """websocketframeFrameHashDevice: adds the decoded batch's output hash into out (int64 CUDA
+    tensor, one element, u64 wrap-around)"""
+    rc = load_bench_lib().websocketframeFrameHashDevice(_ptr(buf), _ptr(desc), _ptr(res), nseg, max_frames, _ptr(out),
+                                                        _stream(stream))
+    check_bench(rc, "websocketframeFrameHashDevice")
 
 
 def set_option(name, value):
