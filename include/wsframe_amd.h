@@ -171,10 +171,12 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, uns
  * Segment offsets are relative to h_buf. Pipelined: groups of consecutive
  * ascending segments (~64 MiB, option "host_chunk_mb") are copied H2D, decoded
  * and copied back D2H on three streams, so both copy directions and the kernel
- * overlap; any other segment layout is one group. Pass pinned memory
+ * overlap; any other segment layout is one group. Only segment bytes are written
+ * back to h_buf (bytes between segments are read, never written). Pass pinned memory
  * (hipHostMalloc / hipHostRegister) for asynchronous DMA; pageable memory works
  * through the runtime's staging copies. h_desc must hold nseg*max_frames
- * descriptors (desc_base form not offered); slots past n_frames are zeroed. */
+ * descriptors (desc_base form not offered); slots past n_frames are zeroed. The
+ * calling thread's current HIP device is unchanged on return. */
 WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
                                                      const unsigned long long* h_seg_off,
                                                      const unsigned long long* h_seg_len, unsigned int nseg,

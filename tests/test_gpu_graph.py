@@ -65,3 +65,44 @@ def test_batch_decode_graph_replay(dev, case):
     g.replay()                                                # XOR again: the wire comes back
     torch.cuda.synchronize()
     assert torch.equal(d[:n], src)
+
+
+def test_two_graphs_replayed_concurrently(dev):
+    """torch captures every graph on one shared capture stream: each captured decode must own
+    its workspace (slots keyed by capture id), so two graphs replayed at the same time on two
+    streams decode their own batches correctly"""
+    def setup(seed):
+        wire, off, pl, plain = wsynth.make_batch(16 * 4096, wsynth.PLEN_MIX3, 0, wsynth.B0_BINARY, seed)
+        so = [int(off[i]) for i in range(0, 16 * 4096, 16)]
+        ends = so[1:] + [len(wire)]
+        sl = [e - s for s, e in zip(so, ends)]
+        n = len(wire)
+        d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+        src = torch.from_numpy(wire).to(dev)
+        t = dict(d=d, src=src, n=n, wire=wire, so=so, sl=sl, plain=plain,
+                 so_t=torch.tensor(so, dtype=torch.int64, device=dev),
+                 sl_t=torch.tensor(sl, dtype=torch.int64, device=dev),
+                 desc=torch.zeros(len(so) * 16 * 32, dtype=torch.uint8, device=dev),
+                 res=torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev))
+        d[:n].copy_(src)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            W.batch_decode_device(d, t["so_t"], t["sl_t"], 16, t["desc"], t["res"])
+        t["g"] = g
+        return t
+    a, b = setup(51), setup(52)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    for rnd in range(4):
+        for t in (a, b):
+            t["d"][:t["n"]].copy_(t["src"])
+            t["res"].zero_()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            a["g"].replay()
+        with torch.cuda.stream(s2):
+            b["g"].replay()
+        torch.cuda.synchronize()
+        for t in (a, b):
+            assert np.array_equal(t["d"][:t["n"]].cpu().numpy(), t["plain"]), rnd
+            r = t["res"].cpu().numpy().view(W.SEGRES_DTYPE)
+            assert int(r["n_frames"].sum()) == 16 * 4096 and int(r["consumed"].sum()) == t["n"], rnd

@@ -401,3 +401,33 @@ def test_strong_scaling_hash_independent_of_rounds(decode_path):
     assert outs[0]["output_hash"] == outs[1]["output_hash"]
     assert outs[0]["allreduced"]["frames"] == outs[1]["allreduced"]["frames"] == 65536
     assert outs[1]["config"]["rounds_per_rank"] == 4
+
+
+def test_host_path_never_writes_between_segments(dev, decode_path):
+    """websocketframeBatchDecodeHost writes back only segment bytes: a read-only page between
+    two segments (another connection's inbuf) stays untouched (a write would fault)"""
+    import ctypes
+    import mmap
+    if decode_path != -1:
+        pytest.skip("host path: one decode path is enough")
+    page = mmap.PAGESIZE
+    mm = mmap.mmap(-1, 3 * page, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+    buf = np.frombuffer(mm, dtype=np.uint8)
+    wire, off, pl, plain = wsynth.make_batch(4, wsynth.PLEN_FIXED, 1000, wsynth.B0_BINARY, 61)
+    a = int(off[2])
+    buf[:a] = wire[:a]                                     # segment 0: frames 0-1, page 0
+    buf[2 * page:2 * page + len(wire) - a] = wire[a:]      # segment 1: frames 2-3, page 2
+    buf[page:2 * page] = 0xA5                              # the gap: page 1, made read-only
+    libc = ctypes.CDLL(None)
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(mm)) + page
+    assert libc.mprotect(ctypes.c_void_p(addr), ctypes.c_size_t(page), 1) == 0      # PROT_READ
+    try:
+        so = np.array([0, 2 * page], np.uint64)
+        sl = np.array([a, len(wire) - a], np.uint64)
+        gd, gr = W.batch_decode_host(buf, so, sl, 4)
+    finally:
+        libc.mprotect(ctypes.c_void_p(addr), ctypes.c_size_t(page), 3)                 # PROT_READ|WRITE
+    assert int(gr["n_frames"].sum()) == 4
+    assert np.array_equal(buf[:a], plain[:a]) and np.array_equal(buf[2 * page:2 * page + len(wire) - a], plain[a:])
+    assert (buf[page:2 * page] == 0xA5).all()
+    del buf

@@ -8,6 +8,11 @@
 //
 // The device slot is addressed as d_slot - lo, so the kernel sees the caller's own
 // segment offsets and writes descriptors with buffer-relative offsets directly.
+// Only segment bytes are copied back (adjacent segments merged into one copy): host bytes
+// between segments are read by the H2D copy of a group's span but never written, so a
+// neighbouring inbuf that another thread is filling meanwhile is left alone. The calling
+// thread's current HIP device is restored before returning.
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -55,6 +60,12 @@ struct Group {
     u64 lo, hi;   // host byte span [lo, hi)
 };
 
+struct DeviceGuard {          // restores the calling thread's current device on every return
+    int dev = -1;
+    DeviceGuard() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+    ~DeviceGuard() { if (dev >= 0) (void)hipSetDevice(dev); }
+};
+
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsigned long long buflen,
                                                                 const u64* h_seg_off, const u64* h_seg_len,
                                                                 unsigned int nseg, unsigned int max_frames,
@@ -64,6 +75,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
     if (!h_buf || !h_seg_off || !h_seg_len || !h_desc || !h_res || max_frames == 0)
         return ws_set_msg("websocketframeBatchDecodeHost: invalid argument");
     if (device < 0 || device >= WS_HOST_DEV) return ws_set_err("device index", hipErrorInvalidDevice);
+    DeviceGuard guard;
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return ws_set_err("hipSetDevice", e);
 
@@ -95,6 +107,23 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
             }
             groups.push_back(g);
             s = g.s1;
+        }
+    }
+    // the host ranges written back per group: its segments' bytes, in buffer order, adjacent
+    // segments merged
+    std::vector<std::vector<std::pair<u64, u64>>> back(groups.size());
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        const Group& g = groups[gi];
+        std::vector<std::pair<u64, u64>> r;
+        r.reserve(g.s1 - g.s0);
+        for (u32 s = g.s0; s < g.s1; ++s)
+            if (h_seg_len[s]) r.emplace_back(h_seg_off[s], h_seg_off[s] + h_seg_len[s]);
+        if (!ordered) std::sort(r.begin(), r.end());
+        for (const auto& x : r) {
+            if (!back[gi].empty() && x.first <= back[gi].back().second)
+                back[gi].back().second = std::max(back[gi].back().second, x.second);
+            else
+                back[gi].push_back(x);
         }
     }
     size_t max_span = 0, max_nseg = 0;
@@ -138,7 +167,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h
         rc = ws_decode_range(S.buf - g.lo, g.lo, g.hi, S.segs, S.segs + S.seg_cap / 2, n, max_frames, nullptr, S.desc,
                              S.res, S.st, S.ws, S.ws_cap);
         if (rc) goto drain;
-        WS_TRY(hipMemcpyAsync(h_buf + g.lo, S.buf, span, hipMemcpyDeviceToHost, S.st), "D2H batch");
+        for (const auto& x : back[gi])
+            WS_TRY(hipMemcpyAsync(h_buf + x.first, S.buf + (x.first - g.lo), x.second - x.first, hipMemcpyDeviceToHost,
+                                  S.st), "D2H batch");
         WS_TRY(hipMemcpyAsync(h_desc + (size_t)g.s0 * max_frames, S.desc, nd * sizeof(WebsocketFrameDesc_t),
                               hipMemcpyDeviceToHost, S.st), "D2H desc");
         WS_TRY(hipMemcpyAsync(h_res + g.s0, S.res, n * sizeof(WebsocketSegResult_t), hipMemcpyDeviceToHost, S.st),

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned c
     const u64 so = seg_off[s], sl = seg_len[s];
     const u64 prev_end = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
     // out of order, or outside the declared range: the gated walker decodes the batch instead
-    if (prev_end > so || so < lo || sl > hi - so) *gptr<u32>(disorder) = gen;
+    if (prev_end > so || so < lo || so > hi || sl > hi - so) *gptr<u32>(disorder) = gen;
     const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
     const u64 ibase = (u64)s * max_frames;
     const u64 sorg = so + lead0;                                            // origin-relative segment start
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     const u64 pend = hi + lead0 ? ((hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
     const u64 so = seg_off[sc], sl = seg_len[sc];
     const u64 prev_end = sc ? seg_off[sc - 1] + seg_len[sc - 1] : 0;
-    if (active && gl == 0 && (prev_end > so || so < lo || sl > hi - so)) *gptr<u32>(disorder) = gen;
+    if (active && gl == 0 && (prev_end > so || so < lo || so > hi || sl > hi - so)) *gptr<u32>(disorder) = gen;
     const u64 dbase = desc_base ? desc_base[sc] : (u64)sc * max_frames;
     const u64 ibase = (u64)sc * max_frames;
     const u64 sorg = so + lead0;
