@@ -366,9 +366,10 @@ def reasm_fused(wl):
 def run_stream(args, dev, world, rank):
     """The batch's wire as ONE raw rx stream (a single connection's inbuf, no frame or
     segment offsets from the host): websocketframeStreamDecodeDevice finds the frame
-    boundaries on the device (speculative grid-wide passes, one 8-byte read per pass) and
-    unmasks with the piece kernel. Same algorithmic bytes as the decode; the call
-    synchronizes its stream (the pass loop reads back the stop word)."""
+    boundaries on the device (speculative grid-wide passes whose loop state stays on the
+    device) and unmasks with the piece kernel. Same algorithmic bytes as the decode. An
+    eager call on a stream this long reads the pass state back once per group of rounds;
+    --graph replays one captured call (no host reads at all)."""
     import torch
     from util_amd import dist as D
     from util_amd import wsframe as W
@@ -376,8 +377,19 @@ def run_stream(args, dev, world, rank):
     wl = Workload.make(args.config, dev, nframes=args.frames, first_frame=rank * nfr)
     res = torch.zeros(16, dtype=torch.uint8, device=dev)
 
-    def step():
+    def call():
         W.stream_decode_device(wl.buf, wl.wire_bytes, wl.nframes, wl.desc, res)
+    graph = None
+    if args.graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            call()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            call()
         wl.decodes += 1
     for _ in range(args.warmup):
         step()
@@ -397,13 +409,14 @@ def run_stream(args, dev, world, rank):
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
         "config": {"workload": "one stream: " + Workload.DESCRIPTION[args.config], "config": args.config,
-                   "frames_per_gpu": wl.nframes, "wire_bytes_per_gpu": wl.wire_bytes,
+                   "hip_graph": args.graph, "frames_per_gpu": wl.nframes, "wire_bytes_per_gpu": wl.wire_bytes,
                    "payload_bytes_per_gpu": wl.payload_bytes},
         "roofline": {"bound": "hbm", "achieved": round(wl.algo_bytes / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
                      "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_launch": wl.algo_bytes,
-                     "timed": "HIP events at the two ends of the timed region / steps: ws_stream_pass_kernel "
-                              "passes (host reads the stop word after each) + ws_piece_unmask_kernel",
+                     "timed": "HIP events at the two ends of the timed region / steps: ws_stream_init_kernel, "
+                              "ws_stream_pass_kernel rounds (state on the device), ws_stream_finish_kernel (gated) "
+                              "+ ws_piece_unmask_kernel",
                      "kernel_ms_mean": round(step_ms, 4)},
         "verified": mism == 0,
         "cpu_baseline": None,

@@ -187,12 +187,16 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
  * host): identical results to websocketframeBatchDecodeDevice with the one segment
  * [0, len) (descriptors d_desc[0..], result d_res[0]); WEBSOCKET_BATCH_PAD readable bytes
  * after d_buf + len. Frame boundaries are found by grid-wide speculative passes (one
- * probe + rest pair per change of frame length, each ends with a small device-to-host
- * read), so the call synchronizes hip_stream; streams whose lengths keep changing finish
- * in a chunk-parallel walk (>= 512 KiB and >= 256 frames left: speculative chunk entries,
- * chunks of ~1024 mean frames up to 8 MiB, each written by one wavefront) or a
- * single-wavefront walk. Scratch memory grows on demand per device (not thread-safe
- * against concurrent calls on one device). Returns 0 or a negative error. */
+ * probe + rest pair per change of frame length); the loop's state stays on the device (the
+ * last block of each pass applies its stop), so the call is asynchronous and may be
+ * captured in a HIP graph: "stream_rounds" pass pairs (default 4), then one wavefront
+ * walks whatever is left. An eager call on a stream of >= 512 KiB reads the state back
+ * after every such group of rounds (one small device-to-host copy, synchronizing
+ * hip_stream): more rounds while they pay, and once lengths keep changing (>= 512 KiB and
+ * >= 256 frames left) a chunk-parallel walk (speculative chunk entries, chunks of ~1024
+ * mean frames up to 8 MiB, each written by one wavefront). Workspace and scratch are per
+ * (stream, graph capture), so calls on different streams may overlap. Returns 0 or a
+ * negative error. */
 WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,
                                                         unsigned int max_frames, WebsocketFrameDesc_t* d_desc,
                                                         WebsocketSegResult_t* d_res, void* hip_stream);

@@ -106,3 +106,82 @@ def test_two_graphs_replayed_concurrently(dev):
             assert np.array_equal(t["d"][:t["n"]].cpu().numpy(), t["plain"]), rnd
             r = t["res"].cpu().numpy().view(W.SEGRES_DTYPE)
             assert int(r["n_frames"].sum()) == 16 * 4096 and int(r["consumed"].sum()) == t["n"], rnd
+
+
+def _streams():
+    w, *_ = wsynth.make_batch(20000, 0, 4096, 0, 3)
+    yield "uniform", w, 1 << 15
+    parts = []
+    for i, (n, fl) in enumerate([(3000, 125), (700, 1500), (40, 65536), (1, 7), (5000, 0), (900, 300)]):
+        parts.append(wsynth.make_batch(n, 0, fl, 0, 10 + i)[0])
+    yield "runs", np.concatenate(parts), 1 << 14             # more length changes than pass rounds
+    wire, so, sl = random_stream(np.random.default_rng(43), 300)
+    yield "random", wire, 4096                                # lengths change every frame: the walk
+    w, *_ = wsynth.make_batch(5000, 0, 1000, 0, 4)
+    yield "max_frames", w, 1234
+
+
+@pytest.mark.parametrize("case", ["uniform", "runs", "random", "max_frames"])
+def test_stream_decode_graph_replay(dev, case):
+    """websocketframeStreamDecodeDevice captured in a graph: the pass loop's state lives on
+    the device (no host reads), so the captured decode replays bit-exact"""
+    name, wire, mf = next(s for s in _streams() if s[0] == case)
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(wire).to(dev)
+    desc = torch.zeros(mf * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(16, dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        W.stream_decode_device(d, n, mf, desc, res)
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, [0], [n], mf)
+    for rnd in range(3):
+        d[:n].copy_(src)
+        desc.zero_()
+        res.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+        assert tuple(gr) == tuple(orr[0]), (rnd, gr, orr[0])
+        gd = desc.cpu().numpy().view(W.DESC_DTYPE)[:int(gr["n_frames"])]
+        assert np.array_equal(gd, od[:int(orr[0]["n_frames"])]), rnd
+        assert np.array_equal(d[:n].cpu().numpy(), ob), rnd
+
+
+FIRST_CALL = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import wsynth
+from oracle_lib import oracle_segments
+from util_amd import wsframe as W
+dev = torch.device("cuda:0")
+wire, *_ = wsynth.make_batch(3000, 0, 1000, 0, 7)
+n = len(wire)
+d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+src = torch.from_numpy(wire).to(dev)
+desc = torch.zeros(4096 * 32, dtype=torch.uint8, device=dev)
+res = torch.zeros(16, dtype=torch.uint8, device=dev)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):                       # the process's first call into the library
+    W.stream_decode_device(d, n, 4096, desc, res)
+d[:n].copy_(src)
+g.replay()
+torch.cuda.synchronize()
+ob = wire.copy()
+od, orr = oracle_segments(ob, [0], [n], 4096)
+assert tuple(res.cpu().numpy().view(W.SEGRES_DTYPE)[0]) == tuple(orr[0])
+assert np.array_equal(d[:n].cpu().numpy(), ob)
+print("OK")
+"""
+
+
+def test_first_library_call_inside_capture(dev):
+    """the per-device state is created by whichever call comes first, a captured one too"""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", FIRST_CALL, here, os.path.dirname(here)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-2000:]

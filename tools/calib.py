@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--modes", default="", help="comma list of mode[:blocks]")
     args = ap.parse_args()
     import torch
-    from util_amd import load_lib
+    from util_amd._lib import load_bench_lib as load_lib
     lib = load_lib()
     n = args.bytes // 16 * 16
     a = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")

@@ -6,7 +6,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from util_amd import load_lib  # noqa: E402
+from util_amd._lib import load_bench_lib as load_lib  # noqa: E402
 
 lib = load_lib()
 n = 4303355904 // 16 * 16

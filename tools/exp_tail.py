@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     args = ap.parse_args()
     import torch
-    from util_amd import load_lib
+    from util_amd._lib import load_bench_lib as load_lib
     lib = load_lib()
     n = args.bytes // 16384 * 16384
     a = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")

@@ -39,7 +39,7 @@ extern WsOpt ws_piece_wn;
 extern WsOpt ws_enc_win;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_reasm_merge;
-extern WsOpt ws_stream_rw, ws_stream_rw_cmax;
+extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
 int ws_set_err(const char* what, hipError_t e) {
@@ -107,6 +107,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
     else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
     else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
+    else if (!strcmp(name, "stream_rounds")) ws_stream_rounds = (int)value;
     else return -1;
     return 0;
 }
@@ -142,6 +143,10 @@ struct WsStreamWs {
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
+    void* aws = nullptr;           // auxiliary device scratch (the stream path's chunk-parallel walk)
+    size_t aws_bytes = 0;
+    void* hws = nullptr;           // ... and its pinned host copy
+    size_t hws_bytes = 0;
 };
 struct WsDevState {
     int init = 0;
@@ -165,8 +170,18 @@ static int dev_state(WsDevState** out) {
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return ws_set_err("hipGetDeviceProperties", e);
         st.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-        if ((e = hipMalloc(&st.ctr, WS_CTR_RING * 128)) != hipSuccess) return ws_set_err("hipMalloc(counters)", e);
-        if ((e = hipMemset(st.ctr, 0, WS_CTR_RING * 128)) != hipSuccess) return ws_set_err("hipMemset(counters)", e);
+        // the first call may come while the thread's stream captures a graph: allocate in
+        // relaxed mode and clear on a private non-blocking stream (neither is part of the graph)
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        hipStream_t ps = nullptr;
+        e = hipMalloc(&st.ctr, WS_CTR_RING * 128);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemsetAsync(st.ctr, 0, WS_CTR_RING * 128, ps);
+        if (e == hipSuccess) e = hipStreamSynchronize(ps);
+        if (ps) (void)hipStreamDestroy(ps);
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        if (e != hipSuccess) return ws_set_err("counters", e);
         st.init = 1;
     }
     *out = &st;
@@ -270,6 +285,35 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     *out = w->ews;
     return 0;
 }
+
+// auxiliary scratch (ws_stream.hip): device part grown like the workspaces, pinned host part
+// grown after draining the stream (eager calls only: a capturing stream cannot drain)
+int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, void** d, void** h) {
+    WsDevState* ds = nullptr;
+    int rc = dev_state(&ds);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    WsStreamWs* w = nullptr;
+    if ((rc = stream_slot(ds, stream, &w))) return rc;
+    if ((rc = grow(&w->aws, &w->aws_bytes, dbytes, stream, 0, "hipMalloc(aux workspace)"))) return rc;
+    if (w->hws_bytes < hbytes) {
+        if (capturing(stream)) return ws_set_msg("aux host scratch cannot grow while the stream captures a graph");
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+        if (w->hws) (void)hipHostFree(w->hws);
+        w->hws = nullptr;
+        w->hws_bytes = 0;
+        const size_t sz = hbytes + hbytes / 4 + 4096;
+        if ((e = hipHostMalloc(&w->hws, sz, hipHostMallocDefault)) != hipSuccess)
+            return ws_set_err("hipHostMalloc(aux scratch)", e);
+        w->hws_bytes = sz;
+    }
+    *d = w->aws;
+    *h = w->hws;
+    return 0;
+}
+
+bool ws_capturing(hipStream_t stream) { return capturing(stream); }
 
 // per-call generation number for the piece path's disorder word (never 0)
 u32 ws_next_gen() {

@@ -322,6 +322,9 @@ struct PieceWs {          // ws_piece.hip workspace views after K1
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out);
 u32 ws_next_gen();
 int ws_device_workspace(size_t bytes, hipStream_t stream, void** out);
+// the calling stream's auxiliary workspace: device scratch + pinned host scratch (eager calls)
+int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, void** d, void** h);
+bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
                     bool* fallback_needed);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`

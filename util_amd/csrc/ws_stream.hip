@@ -69,61 +69,165 @@ __device__ __forceinline__ void stream_pass_one(const unsigned char* __restrict_
     }
 }
 
-// Candidates k in [k0, K), grid-stride. gate != nullptr: a pass launched right behind the
-// probe pass (same stream) that runs only if the probe confirmed all of its candidates.
-// g == 0: the stride is the length of the frame at P (every thread parses it; 0 when it
-// is not a complete frame with a positive return, then only candidate 0 exists), and
-// the candidate count is min(K, what fits the stream and max_frames); block 0 reports
-// {g, candidates} in gk.
+// The pass loop's state, device-resident (in the call's workspace): the host never reads
+// it in a captured call, so a decode of any stream is one asynchronous launch sequence.
+#define SD_PASSES 0u      // the grid passes go on
+#define SD_WALK 1u        // lengths keep changing: the rest is walked (chunk-parallel or one wavefront)
+#define SD_DONE 2u        // result, item count and tail pointers are written
+#define SD_PROBE_K 4096ull
+#define SD_KMAX (1ull << 26)
+struct SdState {
+    u64 P;                           // next frame offset (every frame before it is confirmed)
+    u64 g;                           // the last confirmed frame's length
+    unsigned long long stop[2];      // pass A / pass B: packed first stop (~0: none)
+    u32 ticket[2];                   // blocks of pass A / B done (the last one resolves)
+    u32 nf, extra, short_passes, phase;
+    int status;
+};
+static_assert(sizeof(SdState) <= 128, "stream state");
+
+__global__ void ws_stream_init_kernel(SdState* __restrict__ sd, u64* __restrict__ seg, u64 len,
+                                      u32* __restrict__ disorder) {
+    seg[0] = 0;
+    seg[1] = len;
+    sd->P = 0;
+    sd->g = 0;
+    sd->stop[0] = sd->stop[1] = ~0ull;
+    sd->ticket[0] = sd->ticket[1] = 0;
+    sd->nf = sd->extra = sd->short_passes = 0;
+    sd->phase = SD_PASSES;
+    sd->status = WEBSOCKET_SEG_OK;
+    *disorder = 0;
+}
+
+// the stride at P: the length of the frame there (0 when it is not a complete frame with a
+// positive return: then only candidate 0 exists), and the candidate count of a pass
+__device__ __forceinline__ void sd_stride(const unsigned char* __restrict__ buf, u64 len, u64 P, u32 nf,
+                                          u32 max_frames, u64& g, u64& K) {
+    g = 0;
+    if (P < len && len - P >= 2) {
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + P);
+        const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+        u64 h0, h1;
+        ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+        const WsHdr h = ws_parse(h0, h1, len - P);
+        if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
+    }
+    u64 kf = g ? (len - P) / g + 1 : 1;
+    if (kf > (u64)max_frames - nf + 1) kf = (u64)max_frames - nf + 1;
+    K = kf < SD_KMAX ? kf : SD_KMAX;
+}
+
+// One pass of the loop: part 0 (A) takes candidates [0, SD_PROBE_K), part 1 (B) the rest
+// and runs only if A confirmed all of its candidates. From the last confirmed frame
+// (P, nf) thread k parses the header at P + k*g (g: the length of the frame at P);
+// candidates are ordered, so the pair is exactly one pass over [0, K).
 __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned char* __restrict__ buf, u64 len,
-                                                                 u64 P, u64 g, u32 nf, u32 max_frames, u64 k0, u64 K,
+                                                                 u32 max_frames, int part,
                                                                  WebsocketFrameDesc_t* __restrict__ desc,
                                                                  u32x4* __restrict__ items, u64* __restrict__ ptr,
-                                                                 u64 pend, unsigned long long* __restrict__ stop,
-                                                                 const unsigned long long* __restrict__ gate,
-                                                                 u64* __restrict__ gk) {
-    if (gate && *gate != ~0ull) return;
-    if (g == 0) {
-        if (P < len && len - P >= 2) {
-            const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + P);
+                                                                 u64 pend, SdState* __restrict__ sd) {
+    if (sd->phase != SD_PASSES || (part == 1 && sd->stop[0] != ~0ull)) return;   // the same for every block
+    const u64 P = sd->P;
+    const u32 nf = sd->nf;
+    u64 g, K;
+    sd_stride(buf, len, P, nf, max_frames, g, K);
+    const u64 k0 = part ? SD_PROBE_K : 0, k1 = part ? K : (K < SD_PROBE_K ? K : SD_PROBE_K);
+    for (u64 k = k0 + (u64)blockIdx.x * SPASS_T + threadIdx.x; k < k1; k += (u64)gridDim.x * SPASS_T)
+        stream_pass_one(buf, len, P, g, nf, max_frames, k, desc, items, ptr, pend, &sd->stop[part]);
+}
+
+// After a pass pair: its stop applied to the state (the host loop of earlier versions, in
+// net_reactor.c:515-526 order): advance past a run of g-frames, take a frame of another
+// length (a new stride; its pieces point at it again, later candidates may have written
+// them), or end the walk (ret <= 0, not consumed, max frames: the rest of the pieces point
+// past the items) and write the result. A pass that found a new length within its first 64
+// candidates twice hands the rest to a walk (SD_WALK). Every block derives the same
+// outcome and writes its share of the piece pointers; the last block to finish (ticket)
+// writes the state, after every block has read it.
+__global__ __launch_bounds__(SPASS_T) void ws_stream_resolve_kernel(const unsigned char* __restrict__ buf, u64 len,
+                                                                    u32 max_frames, u64* __restrict__ ptr, u64 pend,
+                                                                    SdState* __restrict__ sd, u32* __restrict__ nwork,
+                                                                    WebsocketSegResult_t* __restrict__ res) {
+    __shared__ u64 f_lo[2], f_hi[2], f_val[2];
+    __shared__ int s_last;
+    if (sd->phase != SD_PASSES) return;
+    const u64 P = sd->P;
+    const u32 nf = sd->nf;
+    const unsigned long long word = sd->stop[0] != ~0ull ? sd->stop[0] : sd->stop[1];   // candidates are ordered
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    u64 g, K;
+    sd_stride(buf, len, P, nf, max_frames, g, K);
+    u64 P2 = P + K * g, g2 = g;
+    u32 nf2 = nf + (u32)K, extra = 0, short_passes = 0, phase = SD_PASSES;
+    int status = WEBSOCKET_SEG_OK;
+    if (threadIdx.x == 0) {
+        f_lo[0] = f_hi[0] = f_lo[1] = f_hi[1] = 0;
+        f_val[0] = f_val[1] = 0;
+    }
+    __syncthreads();
+    if (word != ~0ull) {
+        const u64 m = word >> 36;
+        const u32 code = (u32)(word >> 34) & 3u, stf = (u32)(word >> 32) & 3u;
+        const int ret = (int)(u32)word;
+        const u64 pos_m = P + m * g;
+        const u64 slot_m = (u64)nf + m;
+        nf2 = nf + (u32)m;
+        P2 = pos_m;
+        short_passes = sd->short_passes;
+        phase = SD_DONE;
+        if (code == 1) {
+            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + pos_m + (u32)ret; f_val[0] = slot_m; }
+            nf2 += 1;
+            P2 = pos_m + (u32)ret;
+            g2 = (u32)ret;
+            if (P2 < len) {                                                  // else: consumed the whole stream
+                phase = SD_PASSES;
+                if (m < 64 && ++short_passes >= 2) phase = SD_WALK;
+            }
+        } else if (code == 2) {                                              // ret <= 0: unmasked, walk ends
+            if (ret != 0) { nf2 += 1; status = WEBSOCKET_SEG_ERR_DECODE; }
+            else extra = 1;
+            // its payload extent: the header at pos_m again (the buffer is not written yet)
+            const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + pos_m);
             const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
             u64 h0, h1;
             ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
-            const WsHdr h = ws_parse(h0, h1, len - P);
-            if (h.kind == WS_PARSE_FRAME && h.ret > 0) g = (u32)h.ret;
-        }
-        u64 kf = g ? (len - P) / g + 1 : 1;
-        if (kf > (u64)max_frames - nf + 1) kf = (u64)max_frames - nf + 1;
-        K = kf < K ? kf : K;
-        if (gk && blockIdx.x == 0 && threadIdx.x == 0) {
-            gk[0] = g;
-            gk[1] = K;
+            const WsHdr h = ws_parse(h0, h1, len - pos_m);
+            const u64 p1 = lead0 + pos_m + h.hdr + (h.masked ? h.plen : 0);
+            if (threadIdx.x == 0) {
+                f_lo[0] = lead0 + pos_m; f_hi[0] = p1; f_val[0] = slot_m;
+                f_lo[1] = p1; f_hi[1] = lead0 + len; f_val[1] = (u64)nf2 + extra;
+            }
+        } else {
+            status = stf == 1 ? WEBSOCKET_SEG_MAX_FRAMES : (stf == 2 ? WEBSOCKET_SEG_ERR_LEN_WRAP : WEBSOCKET_SEG_OK);
+            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + len; f_val[0] = nf2; }
         }
     }
-    for (u64 k = k0 + (u64)blockIdx.x * SPASS_T + threadIdx.x; k < K; k += (u64)gridDim.x * SPASS_T)
-        stream_pass_one(buf, len, P, g, nf, max_frames, k, desc, items, ptr, pend, stop);
-}
-
-
-// Piece pointers [lo, hi) -> val. With lo_from_item / hi_from_item the bound is the
-// payload end (P1, origin-relative) of item `item` instead: the extent of a frame whose
-// length the host does not know (the loop's last frame when it returned <= 0).
-__global__ void ws_stream_ptr_kernel(u64* __restrict__ ptr, u64 pend, u64 lo, u64 hi, u64 val,
-                                     const u32x4* __restrict__ items, u64 item, int lo_from_item, int hi_from_item) {
-    if (lo_from_item || hi_from_item) {
-        const u32x4 it = items[item];
-        const u64 p1 = ((u64)it.z | ((u64)it.w << 32)) & 0xFFFFFFFFFFFFull;
-        if (lo_from_item) lo = p1;
-        if (hi_from_item) hi = p1;
+    __syncthreads();
+    const u64 t0 = (u64)blockIdx.x * SPASS_T + threadIdx.x, ts = (u64)gridDim.x * SPASS_T;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+        for (u64 p = ((f_lo[f] + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + t0; (p << PIECE_SHIFT_S) < f_hi[f] && p < pend;
+             p += ts)
+            ptr[p] = f_val[f];
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&sd->ticket[0], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    sd->ticket[0] = 0;
+    sd->stop[0] = sd->stop[1] = ~0ull;
+    sd->P = P2;
+    sd->g = g2;
+    sd->nf = nf2;
+    sd->short_passes = short_passes;
+    sd->phase = phase;
+    if (phase == SD_DONE) {
+        sd->extra = extra;
+        sd->status = status;
+        nwork[0] = nf2 + extra;
+        ws_store_res(res, P2 < len ? P2 : len, nf2, status);
     }
-    const u64 p0 = (lo + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S;
-    for (u64 p = p0 + threadIdx.x; (p << PIECE_SHIFT_S) < hi && p < pend; p += blockDim.x) ptr[p] = val;
-}
-
-__global__ void ws_stream_res_kernel(u32* __restrict__ nwork, u32 cnt, WebsocketSegResult_t* __restrict__ res,
-                                     u64 consumed, u32 nf, int status) {
-    nwork[0] = cnt;
-    ws_store_res(res, consumed, nf, status);
 }
 
 // Frames of the stream starting in [P0, end) from (P0, nf0, g0) by one wavefront: the group
@@ -219,6 +323,18 @@ __global__ __launch_bounds__(64) void ws_stream_walk_kernel(const unsigned char*
                                                             u32* __restrict__ nwork,
                                                             WebsocketSegResult_t* __restrict__ res) {
     stream_walk(buf, len, P0, g0, nf0, len, true, max_frames, desc, items, ptr, pend, nwork, res, threadIdx.x);
+}
+
+// Whatever the pass rounds left (lengths that keep changing, or rounds used up): one
+// wavefront walks from the state's (P, g, nf) to the end; nothing once the state is done
+__global__ __launch_bounds__(64) void ws_stream_finish_kernel(const unsigned char* __restrict__ buf, u64 len,
+                                                              u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
+                                                              u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
+                                                              u32* __restrict__ nwork,
+                                                              WebsocketSegResult_t* __restrict__ res,
+                                                              SdState* __restrict__ sd) {
+    if (sd->phase == SD_DONE) return;
+    stream_walk(buf, len, sd->P, sd->g, sd->nf, len, true, max_frames, desc, items, ptr, pend, nwork, res, threadIdx.x);
 }
 
 // One chunk [P0, end) walked by one wavefront when the chunk-parallel records have no link
@@ -495,45 +611,20 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
 #define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
 WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
+WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
 
-// grow-only scratch for the chunk-parallel walk (per device): device records + counters,
-// and a pinned host copy of them
+// scratch for the chunk-parallel walk: the calling stream's auxiliary workspace (device
+// records + counters, and a pinned host copy of them), so concurrent calls on different
+// streams never share it (the walk runs in eager calls only)
 struct RwScratch {
     void* d = nullptr;
-    size_t d_bytes = 0;
     void* h = nullptr;
-    size_t h_bytes = 0;
 };
-static RwScratch g_rw[64];
 
-static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch** out) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return ws_set_err("hipGetDevice", e);
-    if (dev < 0 || dev >= 64) return ws_set_err("device index", hipErrorInvalidDevice);
-    RwScratch& s = g_rw[dev];
-    if (s.d_bytes < dbytes || s.h_bytes < hbytes) {
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
-    }
-    if (s.d_bytes < dbytes) {
-        if (s.d) (void)hipFree(s.d);
-        s.d = nullptr;
-        s.d_bytes = 0;
-        if ((e = hipMalloc(&s.d, dbytes)) != hipSuccess) return ws_set_err("hipMalloc(stream scratch)", e);
-        s.d_bytes = dbytes;
-    }
-    if (s.h_bytes < hbytes) {
-        if (s.h) (void)hipHostFree(s.h);
-        s.h = nullptr;
-        s.h_bytes = 0;
-        if ((e = hipHostMalloc(&s.h, hbytes, hipHostMallocDefault)) != hipSuccess)
-            return ws_set_err("hipHostMalloc(stream scratch)", e);
-        s.h_bytes = hbytes;
-    }
-    *out = &s;
-    return 0;
+static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch* out) {
+    return ws_aux_workspace(dbytes, hbytes, st, &out->d, &out->h);
 }
 
 static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
@@ -551,7 +642,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     int rc;
     ws_stat_rw_chunk_walks = 0;
     ws_stat_rw_chunks = 0;
-    RwScratch* S = nullptr;
+    RwScratch S;
     u64* wout = nullptr;       // chunk-walk report (device) and its pinned copy
     u64* ho = nullptr;
     // one chunk [ent, end) by one wavefront: the next entry, or the stream finished
@@ -570,8 +661,8 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     };
     // sample: the first RW_SAMPLE bytes, and the mean wire length
     if ((rc = rw_scratch(256, 256, st, &S))) return rc;
-    wout = reinterpret_cast<u64*>(S->d);
-    ho = reinterpret_cast<u64*>(S->h);
+    wout = reinterpret_cast<u64*>(S.d);
+    ho = reinterpret_cast<u64*>(S.h);
     u64 P1 = 0;
     u32 nf1 = 0;
     if ((rc = chunk_walk(P, nf, P + RW_SAMPLE, P1, nf1))) return rc < 0 ? rc : 0;
@@ -601,8 +692,8 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const size_t b_cand = (size_t)nchunks * capc * 8;
     const size_t b_host = b_recs + b_nrec + b_dx + 256 + b_own;              // copied back
     if ((rc = rw_scratch(256 + b_host + b_tab + b_stg + b_cand, 256 + b_host, st, &S))) return rc;
-    unsigned char* w = reinterpret_cast<unsigned char*>(S->d);
-    unsigned char* hw = reinterpret_cast<unsigned char*>(S->h);
+    unsigned char* w = reinterpret_cast<unsigned char*>(S.d);
+    unsigned char* hw = reinterpret_cast<unsigned char*>(S.h);
     wout = reinterpret_cast<u64*>(w);
     ho = reinterpret_cast<u64*>(hw);
     RwRec* recs = reinterpret_cast<RwRec*>(w + 256);
@@ -719,24 +810,21 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         return ws_set_msg("websocketframeStreamDecodeDevice: d_desc/d_res not 16-B aligned");
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     hipError_t e;
-    // workspace: the piece path's layout for one segment [0, len), plus the stop word and the
-    // segment's (offset, length) pair for the unmask kernel
+    // workspace: the piece path's layout for one segment [0, len), then the pass loop's
+    // state and the segment's (offset, length) pair for the unmask kernel
     const size_t pws = ws_piece_workspace_bytes(len, 1, max_frames);
     void* ws = nullptr;
     int rc = ws_device_workspace(pws + 256, st, &ws);
     if (rc) return rc;
     unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
-    unsigned long long* d_stop = reinterpret_cast<unsigned long long*>(w8 + ((pws + 63) & ~(size_t)63));
-    u64* d_seg = reinterpret_cast<u64*>(d_stop + 4);                        // [0] offset 0, [1] length
-    const u64 seg[2] = {0, len};
-    if ((e = hipMemcpyAsync(d_seg, seg, sizeof(seg), hipMemcpyHostToDevice, st)) != hipSuccess)
-        return ws_set_err("hipMemcpyAsync(segment)", e);
+    SdState* sd = reinterpret_cast<SdState*>(w8 + ((pws + 63) & ~(size_t)63));
+    u64* d_seg = reinterpret_cast<u64*>(reinterpret_cast<unsigned char*>(sd) + 128);   // [0] offset 0, [1] length
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
     L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
     PieceWs Pw;
     const u32 gen = ws_next_gen();
-    // the piece-path views of the workspace (no kernel launched: lo == hi == 0 segments walk)
+    // the piece-path views of the workspace
     {
         const u64 lead0 = reinterpret_cast<uintptr_t>(d_buf) & 15;
         Pw.npieces = len + lead0 ? ((len + lead0 - 1) >> PIECE_SHIFT_S) + 1 : 0;
@@ -750,105 +838,57 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         b = (b + 4 + 15) & ~(size_t)15;
         Pw.items = reinterpret_cast<u32x4*>(w8 + b);
     }
-    const u64 lead0 = reinterpret_cast<uintptr_t>(d_buf) & 15;
-    auto set_ptrs = [&](u64 lo, u64 hi, u64 val, u64 item, int lo_it, int hi_it) -> int {
-        hipLaunchKernelGGL(ws_stream_ptr_kernel, dim3(1), dim3(256), 0, st, Pw.ptr, Pw.npieces, lo, hi, val, Pw.items,
-                           item, lo_it, hi_it);
-        hipError_t e2 = hipGetLastError();
-        return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_ptr_kernel launch", e2);
-    };
-    u64 P = 0, g = 0;
-    u32 nf = 0, extra = 0, short_passes = 0;
-    int status = WEBSOCKET_SEG_OK;
-    bool walked = false;
-    bool probe = true;                       // after a length change: a short pass first (a stream
-                                             // whose lengths keep changing never pays a full one)
-    // stop words [0] probe / single pass, [1] the gated rest; [2..3] the derived {g, K}
-    u64* d_gk = reinterpret_cast<u64*>(d_stop + 2);
-    auto pass = [&](u64 gp, u64 k0, u64 K, unsigned long long* stop, const unsigned long long* gate) -> int {
-        const u64 blocks = std::min<u64>((K - k0 + SPASS_T - 1) / SPASS_T, 8192);   // grid-stride beyond
-        hipLaunchKernelGGL(ws_stream_pass_kernel, dim3((u32)blocks), dim3(SPASS_T), 0, st, d_buf, (u64)len, P, gp, nf,
-                           max_frames, k0, K, d_desc, Pw.items, Pw.ptr, Pw.npieces, stop, gate, d_gk);
+    hipLaunchKernelGGL(ws_stream_init_kernel, dim3(1), dim3(1), 0, st, sd, d_seg, (u64)len, Pw.disorder);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_init_kernel launch", e);
+    // pass B's grid: every candidate a stream of this length and max_frames can have, grid-stride
+    u64 kmax = std::min<u64>(std::min<u64>(len / 2 + 1, (u64)max_frames + 1), SD_KMAX);
+    const u32 b_blocks = (u32)std::max<u64>(1, std::min<u64>((kmax + SPASS_T - 1) / SPASS_T, 8192));
+    auto rounds = [&](int n) -> int {
+        for (int r = 0; r < n; ++r) {
+            hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(SD_PROBE_K / SPASS_T), dim3(SPASS_T), 0, st, d_buf, (u64)len,
+                               max_frames, 0, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd);
+            hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(b_blocks), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
+                               1, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd);
+            hipLaunchKernelGGL(ws_stream_resolve_kernel, dim3(64), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
+                               Pw.ptr, Pw.npieces, sd, Pw.nwork, d_res);
+        }
         const hipError_t e2 = hipGetLastError();
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
-    const u64 KMAX = 1ull << 26, PROBE_K = 1ull << 12;
-    for (;;) {
-        if ((e = hipMemsetAsync(d_stop, 0xFF, 16, st)) != hipSuccess) return ws_set_err("hipMemsetAsync(stop)", e);
-        u64 K;
-        unsigned long long words[4] = {0, 0, 0, 0};
-        if (probe) {
-            // after a length change (and at the start): the stride is the length of the frame
-            // at P, derived on the device; a probe pass of PROBE_K candidates and right behind
-            // it (no host round trip) the rest, gated on the probe's stop word
-            if ((rc = pass(0, 0, PROBE_K, d_stop, nullptr)) || (rc = pass(0, PROBE_K, KMAX, d_stop + 1, d_stop)))
-                return rc;
-        } else {
-            K = g ? (len - P) / g + 1 : 1;                                   // candidates this pass
-            if (K > (u64)max_frames - nf + 1) K = (u64)max_frames - nf + 1;
-            if (K > KMAX) K = KMAX;
-            if ((rc = pass(g, 0, K, d_stop, nullptr))) return rc;
-        }
-        if ((e = hipMemcpyAsync(words, d_stop, probe ? 32 : 16, hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return ws_set_err("hipMemcpyAsync(stop D2H)", e);
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
-        if (probe) {
-            g = words[2];
-            K = words[3];
-            if (words[0] == ~0ull && K <= PROBE_K) words[1] = ~0ull;         // no rest pass ran
-        }
-        const unsigned long long word = words[0] != ~0ull ? words[0] : words[1];   // candidates are ordered
-        if (word == ~0ull) {                                                 // all K candidates were g-frames
-            nf += (u32)K;
-            P += K * g;
-            short_passes = 0;
-            probe = false;
-            continue;
-        }
-        probe = true;
-        const u64 m = word >> 36;
-        const u32 code = (u32)(word >> 34) & 3u, stf = (u32)(word >> 32) & 3u;
-        const int ret = (int)(u32)word;
-        const u64 pos_m = P + m * g;
-        const u64 slot_m = (u64)nf + m;
-        nf += (u32)m;
-        if (code == 1) {
-            // frame m is longer than g: later candidates may have written pointers inside it
-            if ((rc = set_ptrs(lead0 + pos_m, lead0 + pos_m + (u32)ret, slot_m, 0, 0, 0))) return rc;
-            nf += 1;
-            P = pos_m + (u32)ret;
-            g = (u32)ret;
-            if (P >= len) break;                                             // consumed the whole stream
-            if (m < 64 && ++short_passes >= 2) {                             // lengths keep changing:
-                if (ws_stream_rw && len - P >= RW_MIN) {                     // chunk-parallel walk
-                    if ((rc = rw_walk(d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
-                } else {                                                     // one wavefront
-                    hipLaunchKernelGGL(ws_stream_walk_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, P, g, nf,
-                                       max_frames, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
-                    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_walk_kernel launch", e);
-                }
-                walked = true;                                               // it writes result and tail
-                break;
+    const int nr = ws_stream_rounds >= 1 && ws_stream_rounds <= 64 ? (int)ws_stream_rounds : 4;
+    // A captured call (and any stream too short for the chunk-parallel walk) never reads the
+    // state back: `nr` pass rounds, then the gated one-wavefront walk finishes whatever the
+    // rounds left. An eager call that may need the chunk-parallel walk reads the state after
+    // every round (one small device-to-host copy): another round while they pay, the
+    // chunk-parallel walk once lengths keep changing.
+    const bool host_rw = ws_stream_rw && len >= RW_MIN && !ws_capturing(st);
+    if ((rc = rounds(host_rw ? 1 : nr))) return rc;
+    bool finished = false;
+    if (host_rw) {
+        void* dh = nullptr;
+        void* hh = nullptr;
+        if ((rc = ws_aux_workspace(256, 256, st, &dh, &hh))) return rc;
+        SdState* hs = reinterpret_cast<SdState*>(hh);
+        for (;;) {
+            if ((e = hipMemcpyAsync(hs, sd, sizeof(SdState), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipStreamSynchronize(st)) != hipSuccess)
+                return ws_set_err("stream state D2H", e);
+            if (hs->phase == SD_DONE) { finished = true; break; }
+            if (hs->phase == SD_PASSES) {
+                if ((rc = rounds(1))) return rc;
+                continue;
             }
-            continue;
+            if (len - hs->P >= RW_MIN) {                                     // lengths keep changing
+                if ((rc = rw_walk(d_buf, len, hs->P, hs->nf, max_frames, d_desc, Pw, d_res, st))) return rc;
+                finished = true;
+            }
+            break;
         }
-        P = pos_m;
-        if (code == 2) {                                                     // ret <= 0: unmasked, walk ends
-            if (ret != 0) { nf += 1; status = WEBSOCKET_SEG_ERR_DECODE; }
-            else extra = 1;
-            if ((rc = set_ptrs(lead0 + pos_m, 0, slot_m, slot_m, 0, 1))) return rc;       // its payload
-            if ((rc = set_ptrs(0, lead0 + len, (u64)nf + extra, slot_m, 1, 0))) return rc;  // the rest
-        } else {
-            status = stf == 1 ? WEBSOCKET_SEG_MAX_FRAMES : (stf == 2 ? WEBSOCKET_SEG_ERR_LEN_WRAP : WEBSOCKET_SEG_OK);
-            if ((rc = set_ptrs(lead0 + pos_m, lead0 + len, nf, 0, 0, 0))) return rc;
-        }
-        break;
     }
-    if (!walked) {
-        hipLaunchKernelGGL(ws_stream_res_kernel, dim3(1), dim3(1), 0, st, Pw.nwork, nf + extra, d_res,
-                           P < len ? P : (u64)len, nf, status);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_res_kernel launch", e);
+    if (!finished) {
+        hipLaunchKernelGGL(ws_stream_finish_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, max_frames, d_desc,
+                           Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, sd);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_finish_kernel launch", e);
     }
-    if ((e = hipMemsetAsync(Pw.disorder, 0, 4, st)) != hipSuccess) return ws_set_err("hipMemsetAsync", e);
     return ws_launch_piece_unmask(L, Pw, 1, gen);
 }

@@ -151,7 +151,8 @@ def batch_decode_device(buf, seg_off, seg_len, max_frames, desc, res, desc_base=
 
 def stream_decode_device(buf, length, max_frames, desc, res, stream=None):
     """websocketframeStreamDecodeDevice: one raw stream buf[0:length) (uint8 CUDA tensor with
-    >= BATCH_PAD bytes after it), decoded in place; synchronizes `stream`."""
+    >= BATCH_PAD bytes after it), decoded in place; asynchronous on `stream` (graph-capturable;
+    an eager call on a stream of >= 512 KiB reads the pass state back)."""
     assert buf.numel() >= length + BATCH_PAD
     rc = load_lib().websocketframeStreamDecodeDevice(_ptr(buf), length, max_frames, _ptr(desc), _ptr(res),
                                                      _stream(stream))
