@@ -712,6 +712,8 @@ def run_strong(args, dev, world, rank):
         "roofline": {"bound": "hbm", "achieved": round(algo / world / step_s / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s per GPU", "frac": round(algo / world / step_s / 1e9 / PEAK_HBM_GBS, 4),
                      "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_step": algo,
+                     "algo_bytes_per_launch": per_round * fps * (wirelen + fl),
+                     "kernel_ms_mean": round(step_s * 1e3 / max(1, loc["rounds"]), 4),
                      "timed": "per round: HIP events at the two ends of `steps` back-to-back decode calls; step = "
                               "sum over the rank's rounds, max over ranks (generation, hashing and checks between "
                               "rounds are outside)"},

@@ -181,3 +181,57 @@ def test_channel_glue_layout(tmp_path):
         pytest.skip("reference headers not present (GPU box)")
     _build_run(tmp_path, "channel_layout.c", "channel_layout", ["-I", REF_INC, "-D_GNU_SOURCE", "-Wno-unused-function"],
                "channel_layout ok")
+
+
+class _DecodeResult(C.Structure):          # NetChannelInbufDecodeResult_t (net_channel_ex.h:10-20)
+    _fields_ = [("err", C.c_char), ("incomplete", C.c_char), ("fragment_eof", C.c_char), ("pktype", C.c_char),
+                ("ignore", C.c_char), ("pkseq", C.c_uint), ("decodelen", C.c_uint), ("bodylen", C.c_uint),
+                ("bodyptr", C.c_void_p)]
+
+
+class _Cursor(C.Structure):                 # WebsocketBatchCursor_t (include/wsframe_amd_channel.h)
+    _fields_ = [("desc", C.c_void_p), ("consumed", C.c_ulonglong), ("n_frames", C.c_uint), ("status", C.c_int),
+                ("seg_off", C.c_ulonglong), ("inbuf", C.c_void_p), ("next", C.c_uint)]
+
+
+def _reactor_loop(buf, on_decode):
+    """the reactor loop over one inbuf (net_reactor.c:515-526) with an on_decode glue:
+    what the stream hook sees, as (body offset, bodylen, fragment_eof, pktype, decodelen)"""
+    base = buf.ctypes.data
+    off, out = 0, []
+    while off < len(buf):
+        r = _DecodeResult()
+        on_decode(base + off, len(buf) - off, C.byref(r))
+        if r.err != b"\x00":
+            out.append("err")
+            break
+        if r.incomplete != b"\x00":
+            break
+        out.append(((r.bodyptr or base) - base, r.bodylen, r.fragment_eof, r.pktype, r.decodelen))
+        off += r.decodelen
+    return out, off
+
+
+@pytest.mark.parametrize("case", ["mixed", "overflow_count", "zero_len", "tail"])
+def test_channel_glue_batch_replay(case):
+    """websocketframeOnDecodeBatch replays a batch decode's descriptors (here the oracle's,
+    bit-identical to the GPU's) to the reactor loop exactly as websocketframeOnDecode's
+    per-frame decode drives it: same bodies, lengths, FIN flags, packet types and stop"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import reasm_cases as R
+    from oracle_lib import oracle_segments
+    lib = util_amd.load_lib()
+    lib.websocketframeOnDecodeBatch.restype = None
+    lib.websocketframeOnDecodeBatch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+    wire, _ = R.build(case)
+    single = wire.copy()
+    ref, ref_off = _reactor_loop(single, lambda p, n, r: lib.websocketframeOnDecode(None, p, n, r))
+    batch = wire.copy()
+    od, orr = oracle_segments(batch, [0], [len(batch)], 1 << 16)     # the batch decode, in place
+    desc = np.ascontiguousarray(od[:int(orr[0]["n_frames"])])
+    cur = _Cursor(desc.ctypes.data, int(orr[0]["consumed"]), int(orr[0]["n_frames"]), int(orr[0]["status"]), 0,
+                  batch.ctypes.data, 0)
+    got, got_off = _reactor_loop(batch, lambda p, n, r: lib.websocketframeOnDecodeBatch(C.byref(cur), p, n, r))
+    assert got == ref and got_off == ref_off
+    assert np.array_equal(batch[:ref_off], single[:ref_off])

@@ -1,12 +1,20 @@
 # GPU box: committed evidence for this round — bench line + rocprofv3 kernel stats + PMC
-# passes for the headline decode (cfg2), decode of small segments (cfg5, segfuse), fused
-# reassembly (cfg5) and client encode (cfg2). Summaries: tools/prof_summary.py (on the CPU side).
+# passes per workload (tools/profile.sh). Summaries: tools/prof_all_summary.sh (CPU side).
+#   bash tools/gpu_profile_all.sh r02 [names...]
 set -e
 export TMPDIR=/tmp
-R=${1:-r01}
-bash tools/profile.sh gpurun_out/${R}_piece
-bash tools/profile.sh gpurun_out/${R}_segfuse_cfg5 --config cfg5
-bash tools/profile.sh gpurun_out/${R}_reasm_fused --op reasm --config cfg5
-bash tools/profile.sh gpurun_out/${R}_encode_cfg2 --op encode
-bash tools/profile.sh gpurun_out/${R}_stream_cfg3 --op stream --config cfg3
-for d in piece segfuse_cfg5 reasm_fused encode_cfg2 stream_cfg3; do echo "== $d"; cut -c1-300 gpurun_out/${R}_$d/bench.json; done
+R=${1:-r02}; shift || true
+ALL="piece piece_cfg3 piece_cfg4 segfuse_cfg5 reasm_fused encode_cfg2 stream_cfg2 stream_cfg3"
+for n in ${@:-$ALL}; do
+  case $n in
+    piece)        bash tools/profile.sh gpurun_out/${R}_piece ;;
+    piece_cfg3)   bash tools/profile.sh gpurun_out/${R}_piece_cfg3 --config cfg3 --no-cpu --no-e2e ;;
+    piece_cfg4)   bash tools/profile.sh gpurun_out/${R}_piece_cfg4 --config cfg4 --steps 10 --warmup 2 ;;
+    segfuse_cfg5) bash tools/profile.sh gpurun_out/${R}_segfuse_cfg5 --config cfg5 --no-cpu --no-e2e ;;
+    reasm_fused)  bash tools/profile.sh gpurun_out/${R}_reasm_fused --op reasm --config cfg5 ;;
+    encode_cfg2)  bash tools/profile.sh gpurun_out/${R}_encode_cfg2 --op encode ;;
+    stream_cfg2)  bash tools/profile.sh gpurun_out/${R}_stream_cfg2 --op stream --config cfg2 ;;
+    stream_cfg3)  bash tools/profile.sh gpurun_out/${R}_stream_cfg3 --op stream --config cfg3 --steps 20 --warmup 3 ;;
+  esac
+  echo "== $n"; cut -c1-200 gpurun_out/${R}_$n/bench.json
+done

@@ -58,13 +58,15 @@ def main():
         if k == kernel:
             nf, nw = a, b
     bench = json.load(open(os.path.join(src, "bench.json")))
-    algo = bench["roofline"]["algo_bytes_per_launch"]
+    rf = bench["roofline"]
+    algo = rf.get("algo_bytes_per_launch") or rf.get("algo_bytes_per_step")
     rec = {
         "kernel": stats[0]["Name"] if stats else kernel,
         "rocprof_calls": int(stats[0]["Calls"]) if stats else 0,
         "rocprof_avg_ns": float(stats[0]["AverageNs"]) if stats else None,
         "rocprof_min_ns": float(stats[0]["MinNs"]) if stats else None,
-        "bench_kernel_ms_mean": bench["roofline"]["kernel_ms_mean"],
+        "bench_kernel_ms_mean": rf.get("kernel_ms_mean"),
+        "bench_ms_per_step": bench.get("ms_per_step"),
         "kernels_summed": names,
         "per_kernel": per_kernel,
         "per_kernel_avg_ns": {k: v["avg_ns"] for k, v in per_kernel.items()},

@@ -171,8 +171,12 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
                                                             const u32* __restrict__ ptr, unsigned char* __restrict__ dst,
                                                             u64 capacity, u32 npieces, u32 half) {
     const u32 tid = threadIdx.x, lane = tid & 63;
-    const u32 pb = ws_win2(blockIdx.x, half);                                // output piece (two windows)
-    if (pb >= npieces) return;                                               // the odd grid's spare block
+    // output piece: half > 0 two windows (ws_win2); half == ~0u XCD-contiguous (block b runs
+    // on XCD b % 8: XCD x takes pieces [x * ppx, (x + 1) * ppx), so each frame record is
+    // fetched into one XCD's L2 only)
+    const u32 ppx = (npieces + 7) >> 3;
+    const u32 pb = half == ~0u ? (blockIdx.x & 7u) * ppx + (blockIdx.x >> 3) : ws_win2(blockIdx.x, half);
+    if (pb >= npieces) return;                                               // the spare blocks
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
@@ -364,7 +368,8 @@ static int enc_side(EncSide** out) {
 }
 WsOpt ws_encode_fused{0}; // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
                           // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
-WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (ws_win2; measured 1 % slower)
+WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (1, ws_win2; measured 1 % slower)
+                          // or XCD-contiguous (2)
 WsOpt ws_encode_side{0};  // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
                           // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
@@ -407,8 +412,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     if (npieces) {
         auto copy = ws_encode_fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
-        const u32 half = ws_enc_win && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0;
-        hipLaunchKernelGGL(copy, dim3(half ? 2 * half : (u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
+        const int win = ws_enc_win;
+        const u32 half = win == 2 ? ~0u : (win == 1 && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0);
+        const u32 grid = win == 2 ? (u32)(((npieces + 7) >> 3) << 3) : (half ? 2 * half : (u32)npieces);
+        hipLaunchKernelGGL(copy, dim3(grid), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
                            d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, half);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
