@@ -299,6 +299,74 @@ __global__ __launch_bounds__(256) void ws_calib_windows_kernel(gu32x4* __restric
         if (i + 256u * u < n) st16<1>(v[u] ^ key, a + i + 256u * u);
 }
 
+// mode 76: as 72, but each wave's four loads cover 4 KiB of consecutive chunks (K2's
+// layout: wave w of the block takes chunks [w*256, w*256 + 256) of its piece) instead of
+// four 1 KiB rows 4 KiB apart
+__global__ __launch_bounds__(256) void ws_calib_windows_wc_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw,
+                                                                  u32 key) {
+    const u64 npieces = (n + 1023) / 1024, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u64 i = piece * 1024 + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
+}
+
+// modes 73-75: the segment-kernel shape (segfuse / fused reassembly) without frame logic:
+// one 256-thread block per "segment" of `segc` 16-B chunks (cfg5: 1032), segments taken in
+// two windows (ws_win2), in-place XOR. 73: LDS-DMA of the segment (1 KiB slices by every
+// wave), barrier, XOR from LDS, store (segfuse's data path); 74: the segment in registers
+// (U chunks per lane), XOR, store (K2's data path at segment granularity); 75: as 74 plus a
+// copy of the registers into LDS and a barrier before the stores (what a register-resident
+// segment kernel needs for its walk).
+typedef __attribute__((address_space(3))) void ws_lds_void;
+template <int MODE, int U>
+__global__ __launch_bounds__(256) void ws_calib_seg_kernel(gu32x4* __restrict__ a, u64 nseg, u32 segc, u32 half,
+                                                           u32 key) {
+    __shared__ __attribute__((aligned(16))) u32x4 win[U * 256];
+    const u32 b = half ? (blockIdx.x & 1u) * half + (blockIdx.x >> 1) : blockIdx.x;
+    if (b >= nseg) return;
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    gu32x4* const g = a + (u64)b * segc;
+    if (MODE == 73) {
+        const u32 nsl = (segc + 63) / 64;
+        for (u32 i = wv; i < nsl; i += 4) {
+            const u32 c = i * 64 + lane < segc ? i * 64 + lane : segc - 1;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const WS_GLOBAL void*>(g + c), (ws_lds_void*)(&win[i * 64]),
+                                             16, 0, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32 c = u * 256 + tid;
+            if (c < segc) st16<1>(win[c] ^ key, g + c);
+        }
+    } else {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32 c = u * 256 + tid;
+            v[u] = ld16<1>(g + (c < segc ? c : segc - 1));
+        }
+        if (MODE == 75) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) win[u * 256 + tid] = v[u];
+            __syncthreads();
+            key ^= win[(tid * 7) & (U * 256 - 1)].x & 0u;   // a dependent LDS read (value unused)
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32 c = u * 256 + tid;
+            if (c < segc) st16<1>(v[u] ^ key, g + c);
+        }
+    }
+}
+
 // mode 16+: one-shot in-place XOR through buffer instructions with explicit cache
 // bits (aux: bit0 sc0, bit1 nt, bit4 sc1), T threads x U chunks per block.
 template <int T, int U, int LAUX, int SAUX>
@@ -321,7 +389,6 @@ __global__ __launch_bounds__(T) void ws_calib_buf_kernel(unsigned char* __restri
 // (global_load_lds, D stages of S chunks in flight, never a store, never an LDS read,
 // so its vmcnt waits cover only its own loads); waves 1..NC only read LDS and store
 // (never a global load, so no store ever delays a load). One barrier per stage.
-typedef __attribute__((address_space(3))) void ws_lds_void;
 template <int S, int D, int NC, bool IL>
 __global__ __launch_bounds__(64 * (NC + 1)) void ws_calib_ldspipe_kernel(gu32x4* __restrict__ a, u64 nstages,
                                                                         u32 key) {
@@ -439,6 +506,24 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         hipLaunchKernelGGL(ws_calib_windows_kernel, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_kernel launch", e);
+    }
+    if (mode == 76) {  // `blocks` = number of windows
+        const u32 W = blocks > 0 ? (u32)blocks : 2u;
+        const u64 np = (n + 1023) / 1024, ppw = (np + W - 1) / W;
+        hipLaunchKernelGGL(ws_calib_windows_wc_kernel, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
+    }
+    if (mode >= 73 && mode <= 75) {  // `blocks` = chunks per segment (<= 1280)
+        const u32 segc = blocks > 0 && blocks <= 1280 ? (u32)blocks : 1032u;
+        const u64 nseg = n / segc;
+        const u32 half = nseg >= 512 ? (u32)((nseg + 1) / 2) : 0u;
+        const u32 grid = half ? 2 * half : (u32)nseg;
+        if (mode == 73) hipLaunchKernelGGL((ws_calib_seg_kernel<73, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        if (mode == 74) hipLaunchKernelGGL((ws_calib_seg_kernel<74, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        if (mode == 75) hipLaunchKernelGGL((ws_calib_seg_kernel<75, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_seg_kernel launch", e);
     }
     if (mode == 70 || mode == 71) {  // persistent; d_b's first 4 bytes are the ticket counter
         const u32 nb = blocks > 0 ? (u32)blocks : 2048u;
