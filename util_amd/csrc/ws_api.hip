@@ -37,6 +37,7 @@ int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_scan_win;
 extern WsOpt ws_piece_wn;
 extern WsOpt ws_enc_win;
+extern WsOpt ws_seg_lds;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_reasm_merge;
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
@@ -96,6 +97,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
     else if (!strcmp(name, "piece_win")) ws_piece_win = (int)value;
     else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
+    else if (!strcmp(name, "seg_lds")) ws_seg_lds = (int)value;
     else if (!strcmp(name, "piece_wbit")) ws_piece_wbit = (int)value;
     else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
     else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;

@@ -302,6 +302,7 @@ __global__ __launch_bounds__(256) void ws_calib_windows_kernel(gu32x4* __restric
 // mode 76: as 72, but each wave's four loads cover 4 KiB of consecutive chunks (K2's
 // layout: wave w of the block takes chunks [w*256, w*256 + 256) of its piece) instead of
 // four 1 KiB rows 4 KiB apart
+template <int WAIT>
 __global__ __launch_bounds__(256) void ws_calib_windows_wc_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw,
                                                                   u32 key) {
     const u64 npieces = (n + 1023) / 1024, last = n - 1;
@@ -311,6 +312,9 @@ __global__ __launch_bounds__(256) void ws_calib_windows_wc_kernel(gu32x4* __rest
     u32x4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+    if (WAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every load back before the first store
+    if (WAIT == 2) __builtin_amdgcn_s_sleep(32);                    // then a pause (~2k clocks)
+    if (WAIT == 3) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }   // (~16k clocks)
 #pragma unroll
     for (int u = 0; u < 4; ++u)
         if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
@@ -507,10 +511,24 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_kernel launch", e);
     }
-    if (mode == 76) {  // `blocks` = number of windows
+    if (mode >= 76 && mode <= 82) {  // `blocks` = number of windows; 77/78/79: unused dynamic LDS so that
+                                     // at most 7 / 6 / 5 blocks fit a CU; 80: stores after every load is back;
+                                     // 81 / 82: and after a pause of ~2k / ~16k clocks
         const u32 W = blocks > 0 ? (u32)blocks : 2u;
         const u64 np = (n + 1023) / 1024, ppw = (np + W - 1) / W;
-        hipLaunchKernelGGL(ws_calib_windows_wc_kernel, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw, 0x5A5A5A5Au);
+        const u32 dyn = mode == 77 ? 21u << 10 : (mode == 78 ? 24u << 10 : (mode == 79 ? 30u << 10 : 0u));
+        if (mode == 80)
+            hipLaunchKernelGGL(ws_calib_windows_wc_kernel<1>, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw,
+                               0x5A5A5A5Au);
+        else if (mode == 81)
+            hipLaunchKernelGGL(ws_calib_windows_wc_kernel<2>, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw,
+                               0x5A5A5A5Au);
+        else if (mode == 82)
+            hipLaunchKernelGGL(ws_calib_windows_wc_kernel<3>, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw,
+                               0x5A5A5A5Au);
+        else
+            hipLaunchKernelGGL(ws_calib_windows_wc_kernel<0>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw,
+                               0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
     }

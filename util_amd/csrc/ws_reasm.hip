@@ -263,6 +263,7 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
 // walk state and the body table (max_frames <= RSEG_TB bodies) persist across windows.
 // Each wire byte is read from HBM once (+ 1 KiB of look-ahead per extra window), each
 // body byte written once.
+extern WsOpt ws_seg_lds;
 #define RSEG_T 256
 // window = L LDS-DMA wave instructions of 1 KiB: (L-1) KiB owned + 1 KiB look-ahead;
 // L = 18 is ~20 KB of LDS: 8 workgroups (32 waves) per CU ("reasm_cfg" A/B: ws_reasm_cfg)
@@ -543,7 +544,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     if (fused && max_frames <= RSEG_TB) {
         auto k = rcfg == 1 ? ws_reasm_seg_kernel<18, 1> : (rcfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
         const u32 half = ws_seg_win && nseg >= 512 ? (nseg + 1) / 2 : 0;
-        hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
+        const int dyn = ws_seg_lds;
+        hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), dyn > 0 && dyn <= 65536 ? dyn : 0, st, d_buf,
+                           max_frames, d_seg_off,
                            d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, (u32)ws_reasm_merge,
                            nseg, half, (u32)readcache_max_size, d_cached);
         const hipError_t e = hipGetLastError();

@@ -161,6 +161,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
     if (tid == 0) ws_store_res(res + s, off, nf, status);
 }
 
+WsOpt ws_seg_lds{0};     // "seg_lds": bytes of unused dynamic LDS per segment block (occupancy A/B)
 WsOpt ws_segfuse_cfg{0}; // "segfuse_cfg": 0 256 threads, 17 KiB windows (8 workgroups/CU), 1 256 x 19 KiB,
                           // 2 1024 x 65 KiB (one window per 64 KiB segment), 3 512 x 33 KiB
 
@@ -176,7 +177,9 @@ int ws_launch_segfuse(const WsLaunch& L, int nt) {
         default: k = nt == 1 ? ws_segfuse_kernel<1, 18, 256> : ws_segfuse_kernel<0, 18, 256>;
     }
     const u32 half = ws_seg_win && L.nseg >= 512 ? (L.nseg + 1) / 2 : 0;
-    hipLaunchKernelGGL(k, dim3(half ? 2 * half : L.nseg), dim3(T), 0, L.stream, L.buf, L.seg_off, L.seg_len,
+    const int dyn = ws_seg_lds;                                             // unused LDS: fewer blocks per CU
+    hipLaunchKernelGGL(k, dim3(half ? 2 * half : L.nseg), dim3(T), dyn > 0 && dyn <= 65536 ? dyn : 0, L.stream, L.buf,
+                       L.seg_off, L.seg_len,
                        L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_segfuse_kernel launch", e);
