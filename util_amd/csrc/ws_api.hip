@@ -148,7 +148,9 @@ struct WsStreamWs {
     void* aws = nullptr;           // auxiliary device scratch (the stream path's chunk-parallel walk)
     size_t aws_bytes = 0;
     void* hws = nullptr;           // ... and its pinned host copy
+    void* hws_dev = nullptr;       // (its device address)
     size_t hws_bytes = 0;
+    bool aux_state_ok = false;     // the stream path's state (aux head) rests at zero
 };
 struct WsDevState {
     int init = 0;
@@ -257,8 +259,20 @@ static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, size_t
     e = hipMalloc(p, sz);
     if (cap) (void)hipThreadExchangeStreamCaptureMode(&mode);
     if (e != hipSuccess) return ws_set_err(what, e);
-    if (zero_bytes && (e = hipMemsetAsync(*p, 0, zero_bytes < sz ? zero_bytes : sz, stream)) != hipSuccess)
+    if (zero_bytes && cap) {
+        // not part of the graph: cleared once, on a private stream, in relaxed mode
+        hipStream_t ps = nullptr;
+        hipStreamCaptureMode m2 = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&m2);
+        e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemsetAsync(*p, 0, zero_bytes < sz ? zero_bytes : sz, ps);
+        if (e == hipSuccess) e = hipStreamSynchronize(ps);
+        if (ps) (void)hipStreamDestroy(ps);
+        (void)hipThreadExchangeStreamCaptureMode(&m2);
+        if (e != hipSuccess) return ws_set_err(what, e);
+    } else if (zero_bytes && (e = hipMemsetAsync(*p, 0, zero_bytes < sz ? zero_bytes : sz, stream)) != hipSuccess) {
         return ws_set_err(what, e);
+    }
     *have = sz;
     return 0;
 }
@@ -288,30 +302,42 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
     return 0;
 }
 
-// auxiliary scratch (ws_stream.hip): device part grown like the workspaces, pinned host part
-// grown after draining the stream (eager calls only: a capturing stream cannot drain)
-int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, void** d, void** h) {
+// auxiliary scratch (ws_stream.hip): device part grown like the workspaces, its first
+// WS_AUX_HEAD bytes zeroed at every (re)allocation (the stream path's state rests at zero);
+// a pinned, device-visible host part grown after draining the stream (never while capturing)
+int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, WsAux* out) {
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(g_dev_mu);
     WsStreamWs* w = nullptr;
     if ((rc = stream_slot(ds, stream, &w))) return rc;
-    if ((rc = grow(&w->aws, &w->aws_bytes, dbytes, stream, 0, "hipMalloc(aux workspace)"))) return rc;
+    const void* before = w->aws;
+    const size_t have = w->aws_bytes;
+    if ((rc = grow(&w->aws, &w->aws_bytes, dbytes < WS_AUX_HEAD ? WS_AUX_HEAD : dbytes, stream, WS_AUX_HEAD,
+                   "hipMalloc(aux workspace)")))
+        return rc;
+    if (w->aws != before || w->aws_bytes != have) w->aux_state_ok = true;   // freshly zeroed
     if (w->hws_bytes < hbytes) {
         if (capturing(stream)) return ws_set_msg("aux host scratch cannot grow while the stream captures a graph");
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
         if (w->hws) (void)hipHostFree(w->hws);
         w->hws = nullptr;
+        w->hws_dev = nullptr;
         w->hws_bytes = 0;
         const size_t sz = hbytes + hbytes / 4 + 4096;
-        if ((e = hipHostMalloc(&w->hws, sz, hipHostMallocDefault)) != hipSuccess)
+        if ((e = hipHostMalloc(&w->hws, sz, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return ws_set_err("hipHostMalloc(aux scratch)", e);
+        memset(w->hws, 0, sz);
+        if ((e = hipHostGetDevicePointer(&w->hws_dev, w->hws, 0)) != hipSuccess)
+            return ws_set_err("hipHostGetDevicePointer(aux scratch)", e);
         w->hws_bytes = sz;
     }
-    *d = w->aws;
-    *h = w->hws;
+    out->d = w->aws;
+    out->h = w->hws;
+    out->h_dev = w->hws_dev;
+    out->state_ok = &w->aux_state_ok;
     return 0;
 }
 

@@ -322,8 +322,16 @@ struct PieceWs {          // ws_piece.hip workspace views after K1
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out);
 u32 ws_next_gen();
 int ws_device_workspace(size_t bytes, hipStream_t stream, void** out);
-// the calling stream's auxiliary workspace: device scratch + pinned host scratch (eager calls)
-int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, void** d, void** h);
+// the calling stream's auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are
+// zero at allocation + pinned, device-visible host scratch (eager calls)
+#define WS_AUX_HEAD 256
+struct WsAux {
+    void* d;              // device scratch
+    void* h;              // pinned host scratch (nullptr until requested)
+    void* h_dev;          // its device address
+    bool* state_ok;       // the owner's flag: the head holds a resting state
+};
+int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, WsAux* out);
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
                     bool* fallback_needed);

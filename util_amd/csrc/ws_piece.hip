@@ -267,7 +267,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) { m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0; cov[u] = 0; }
     // no early return: an exit branch here would be hoisted above the payload loads
-    u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv;
+    u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv, step = 16;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
@@ -299,8 +299,10 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
             }
         }
         if (k < cnt) {
+            // items load `step` at a time: 16 first (a 4 KiB wave range rarely needs more), 64
+            // after that — all 64 lanes loading would fetch 1 KiB of items per wave in long segments
             const u32 j = k + lane;
-            const bool valid = j < cnt;
+            const bool valid = j < cnt && lane < step;
             u32x4 q = {0, 0, 0, 0};
             if (valid) q = items[(u64)s * max_frames + j];
             const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
@@ -332,12 +334,13 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                     m[u][3] |= key & nib_to_bytemask(bits >> 12);
                 }
             }
-            if (nlim < 64) break;                                           // reached an item past the range
-            if (k + 64 < cnt) { k += 64; continue; }                        // more items of this segment
+            if (nlim < step) break;                                         // reached an item past the range
+            if (k + step < cnt) { k += step; step = 64; continue; }         // more items of this segment
         }
         // this segment has no more items: continue with the next one if it starts in range
         if (++s >= nseg || seg_off[s] + lead0 >= r1) break;
         k = 0;
+        step = 16;
     }
     // ---- 3. store: full chunks one 16-B store, edge chunks exactly the covered bytes
 #pragma unroll

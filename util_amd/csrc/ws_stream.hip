@@ -65,12 +65,16 @@ __device__ __forceinline__ void stream_pass_one(const unsigned char* __restrict_
     if (code != 0) {
         const unsigned long long word = ((unsigned long long)k << 36) | ((unsigned long long)code << 34) |
                                         ((unsigned long long)stf << 32) | (u32)h.ret;
-        atomicMin(stop, word);
+        atomicMax(stop, ~word);                                              // the first stop, inverted
     }
 }
 
-// The pass loop's state, device-resident (in the call's workspace): the host never reads
-// it in a captured call, so a decode of any stream is one asynchronous launch sequence.
+// The pass loop's state, device-resident (the first bytes of the calling stream's auxiliary
+// workspace): the host never has to read it, so a decode of any stream can be one
+// asynchronous launch sequence. It RESTS at zero between calls — stop words 0 (= no stop:
+// they hold ~word, merged with atomicMax), ticket 0 — so a call needs no init kernel: the
+// first round starts from (P, nf) = (0, 0) without reading it, and every resolve leaves the
+// stop words and the ticket at zero again.
 #define SD_PASSES 0u      // the grid passes go on
 #define SD_WALK 1u        // lengths keep changing: the rest is walked (chunk-parallel or one wavefront)
 #define SD_DONE 2u        // result, item count and tail pointers are written
@@ -79,25 +83,21 @@ __device__ __forceinline__ void stream_pass_one(const unsigned char* __restrict_
 struct SdState {
     u64 P;                           // next frame offset (every frame before it is confirmed)
     u64 g;                           // the last confirmed frame's length
-    unsigned long long stop[2];      // pass A / pass B: packed first stop (~0: none)
-    u32 ticket[2];                   // blocks of pass A / B done (the last one resolves)
+    unsigned long long stop[2];      // pass A / pass B: ~(packed first stop), 0: none
+    u32 ticket;                      // resolve blocks done (the last one writes the state)
     u32 nf, extra, short_passes, phase;
     int status;
 };
 static_assert(sizeof(SdState) <= 128, "stream state");
+struct SdMirror {                    // pinned host copy of the state after a resolve (eager calls)
+    u64 P, g;
+    u32 nf, phase, gen, pad;
+};
 
-__global__ void ws_stream_init_kernel(SdState* __restrict__ sd, u64* __restrict__ seg, u64 len,
-                                      u32* __restrict__ disorder) {
-    seg[0] = 0;
-    seg[1] = len;
-    sd->P = 0;
-    sd->g = 0;
-    sd->stop[0] = sd->stop[1] = ~0ull;
-    sd->ticket[0] = sd->ticket[1] = 0;
-    sd->nf = sd->extra = sd->short_passes = 0;
-    sd->phase = SD_PASSES;
-    sd->status = WEBSOCKET_SEG_OK;
-    *disorder = 0;
+// reset of a state left dirty by a call that failed between its launches (rare)
+__global__ void ws_stream_init_kernel(SdState* __restrict__ sd) {
+    sd->stop[0] = sd->stop[1] = 0;
+    sd->ticket = 0;
 }
 
 // the stride at P: the length of the frame there (0 when it is not a complete frame with a
@@ -121,113 +121,28 @@ __device__ __forceinline__ void sd_stride(const unsigned char* __restrict__ buf,
 // One pass of the loop: part 0 (A) takes candidates [0, SD_PROBE_K), part 1 (B) the rest
 // and runs only if A confirmed all of its candidates. From the last confirmed frame
 // (P, nf) thread k parses the header at P + k*g (g: the length of the frame at P);
-// candidates are ordered, so the pair is exactly one pass over [0, K).
+// candidates are ordered, so the pair is exactly one pass over [0, K). `first`: the call's
+// first round, from (0, 0) — its pass A also writes the unmask's segment pair and clears
+// the unmask's gate word.
 __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned char* __restrict__ buf, u64 len,
-                                                                 u32 max_frames, int part,
+                                                                 u32 max_frames, int part, int first,
                                                                  WebsocketFrameDesc_t* __restrict__ desc,
                                                                  u32x4* __restrict__ items, u64* __restrict__ ptr,
-                                                                 u64 pend, SdState* __restrict__ sd) {
-    if (sd->phase != SD_PASSES || (part == 1 && sd->stop[0] != ~0ull)) return;   // the same for every block
-    const u64 P = sd->P;
-    const u32 nf = sd->nf;
+                                                                 u64 pend, SdState* __restrict__ sd,
+                                                                 u64* __restrict__ seg, u32* __restrict__ disorder) {
+    if (first && part == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        seg[0] = 0;
+        seg[1] = len;
+        *disorder = 0;
+    }
+    if ((!first && sd->phase != SD_PASSES) || (part == 1 && sd->stop[0] != 0)) return;   // the same for every block
+    const u64 P = first ? 0 : sd->P;
+    const u32 nf = first ? 0 : sd->nf;
     u64 g, K;
     sd_stride(buf, len, P, nf, max_frames, g, K);
     const u64 k0 = part ? SD_PROBE_K : 0, k1 = part ? K : (K < SD_PROBE_K ? K : SD_PROBE_K);
     for (u64 k = k0 + (u64)blockIdx.x * SPASS_T + threadIdx.x; k < k1; k += (u64)gridDim.x * SPASS_T)
         stream_pass_one(buf, len, P, g, nf, max_frames, k, desc, items, ptr, pend, &sd->stop[part]);
-}
-
-// After a pass pair: its stop applied to the state (the host loop of earlier versions, in
-// net_reactor.c:515-526 order): advance past a run of g-frames, take a frame of another
-// length (a new stride; its pieces point at it again, later candidates may have written
-// them), or end the walk (ret <= 0, not consumed, max frames: the rest of the pieces point
-// past the items) and write the result. A pass that found a new length within its first 64
-// candidates twice hands the rest to a walk (SD_WALK). Every block derives the same
-// outcome and writes its share of the piece pointers; the last block to finish (ticket)
-// writes the state, after every block has read it.
-__global__ __launch_bounds__(SPASS_T) void ws_stream_resolve_kernel(const unsigned char* __restrict__ buf, u64 len,
-                                                                    u32 max_frames, u64* __restrict__ ptr, u64 pend,
-                                                                    SdState* __restrict__ sd, u32* __restrict__ nwork,
-                                                                    WebsocketSegResult_t* __restrict__ res) {
-    __shared__ u64 f_lo[2], f_hi[2], f_val[2];
-    __shared__ int s_last;
-    if (sd->phase != SD_PASSES) return;
-    const u64 P = sd->P;
-    const u32 nf = sd->nf;
-    const unsigned long long word = sd->stop[0] != ~0ull ? sd->stop[0] : sd->stop[1];   // candidates are ordered
-    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
-    u64 g, K;
-    sd_stride(buf, len, P, nf, max_frames, g, K);
-    u64 P2 = P + K * g, g2 = g;
-    u32 nf2 = nf + (u32)K, extra = 0, short_passes = 0, phase = SD_PASSES;
-    int status = WEBSOCKET_SEG_OK;
-    if (threadIdx.x == 0) {
-        f_lo[0] = f_hi[0] = f_lo[1] = f_hi[1] = 0;
-        f_val[0] = f_val[1] = 0;
-    }
-    __syncthreads();
-    if (word != ~0ull) {
-        const u64 m = word >> 36;
-        const u32 code = (u32)(word >> 34) & 3u, stf = (u32)(word >> 32) & 3u;
-        const int ret = (int)(u32)word;
-        const u64 pos_m = P + m * g;
-        const u64 slot_m = (u64)nf + m;
-        nf2 = nf + (u32)m;
-        P2 = pos_m;
-        short_passes = sd->short_passes;
-        phase = SD_DONE;
-        if (code == 1) {
-            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + pos_m + (u32)ret; f_val[0] = slot_m; }
-            nf2 += 1;
-            P2 = pos_m + (u32)ret;
-            g2 = (u32)ret;
-            if (P2 < len) {                                                  // else: consumed the whole stream
-                phase = SD_PASSES;
-                if (m < 64 && ++short_passes >= 2) phase = SD_WALK;
-            }
-        } else if (code == 2) {                                              // ret <= 0: unmasked, walk ends
-            if (ret != 0) { nf2 += 1; status = WEBSOCKET_SEG_ERR_DECODE; }
-            else extra = 1;
-            // its payload extent: the header at pos_m again (the buffer is not written yet)
-            const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + pos_m);
-            const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-            u64 h0, h1;
-            ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
-            const WsHdr h = ws_parse(h0, h1, len - pos_m);
-            const u64 p1 = lead0 + pos_m + h.hdr + (h.masked ? h.plen : 0);
-            if (threadIdx.x == 0) {
-                f_lo[0] = lead0 + pos_m; f_hi[0] = p1; f_val[0] = slot_m;
-                f_lo[1] = p1; f_hi[1] = lead0 + len; f_val[1] = (u64)nf2 + extra;
-            }
-        } else {
-            status = stf == 1 ? WEBSOCKET_SEG_MAX_FRAMES : (stf == 2 ? WEBSOCKET_SEG_ERR_LEN_WRAP : WEBSOCKET_SEG_OK);
-            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + len; f_val[0] = nf2; }
-        }
-    }
-    __syncthreads();
-    const u64 t0 = (u64)blockIdx.x * SPASS_T + threadIdx.x, ts = (u64)gridDim.x * SPASS_T;
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-        for (u64 p = ((f_lo[f] + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + t0; (p << PIECE_SHIFT_S) < f_hi[f] && p < pend;
-             p += ts)
-            ptr[p] = f_val[f];
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&sd->ticket[0], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last || threadIdx.x != 0) return;
-    sd->ticket[0] = 0;
-    sd->stop[0] = sd->stop[1] = ~0ull;
-    sd->P = P2;
-    sd->g = g2;
-    sd->nf = nf2;
-    sd->short_passes = short_passes;
-    sd->phase = phase;
-    if (phase == SD_DONE) {
-        sd->extra = extra;
-        sd->status = status;
-        nwork[0] = nf2 + extra;
-        ws_store_res(res, P2 < len ? P2 : len, nf2, status);
-    }
 }
 
 // Frames of the stream starting in [P0, end) from (P0, nf0, g0) by one wavefront: the group
@@ -325,14 +240,132 @@ __global__ __launch_bounds__(64) void ws_stream_walk_kernel(const unsigned char*
     stream_walk(buf, len, P0, g0, nf0, len, true, max_frames, desc, items, ptr, pend, nwork, res, threadIdx.x);
 }
 
-// Whatever the pass rounds left (lengths that keep changing, or rounds used up): one
-// wavefront walks from the state's (P, g, nf) to the end; nothing once the state is done
+// After a pass pair: its stop applied to the state (the host loop of earlier versions, in
+// net_reactor.c:515-526 order): advance past a run of g-frames, take a frame of another
+// length (a new stride; its pieces point at it again, later candidates may have written
+// them), or end the walk (ret <= 0, not consumed, max frames: the rest of the pieces point
+// past the items) and write the result. A pass that found a new length within its first 64
+// candidates twice hands the rest to a walk (SD_WALK). Every block derives the same
+// outcome and writes its share of the piece pointers; the last block to finish (ticket)
+// writes the state, after every block has read it, and resets the stop words. `finish`
+// (the last round of a call that does not read the state back): that block's first wave
+// also walks whatever is left, one wavefront from (P, g, nf) to the end. `mirror` (eager
+// calls): the state is published to pinned host memory, tagged with the call's `gen`.
+__global__ __launch_bounds__(SPASS_T) void ws_stream_resolve_kernel(const unsigned char* __restrict__ buf, u64 len,
+                                                                    u32 max_frames, int first, int finish,
+                                                                    WebsocketFrameDesc_t* __restrict__ desc,
+                                                                    u32x4* __restrict__ items, u64* __restrict__ ptr,
+                                                                    u64 pend, SdState* __restrict__ sd,
+                                                                    u32* __restrict__ nwork,
+                                                                    WebsocketSegResult_t* __restrict__ res,
+                                                                    SdMirror* __restrict__ mirror, u32 gen) {
+    __shared__ u64 f_lo[2], f_hi[2], f_val[2];
+    __shared__ int s_last;
+    if (!first && sd->phase != SD_PASSES) {                                  // nothing left to resolve
+        if (finish && blockIdx.x == 0 && threadIdx.x < 64 && sd->phase != SD_DONE)
+            stream_walk(buf, len, sd->P, sd->g, sd->nf, len, true, max_frames, desc, items, ptr, pend, nwork, res,
+                        threadIdx.x);
+        return;
+    }
+    const u64 P = first ? 0 : sd->P;
+    const u32 nf = first ? 0 : sd->nf;
+    const unsigned long long word = sd->stop[0] ? ~sd->stop[0] : ~sd->stop[1];   // candidates are ordered
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    u64 g, K;
+    sd_stride(buf, len, P, nf, max_frames, g, K);
+    u64 P2 = P + K * g, g2 = g;
+    u32 nf2 = nf + (u32)K, extra = 0, short_passes = 0, phase = SD_PASSES;
+    int status = WEBSOCKET_SEG_OK;
+    if (threadIdx.x == 0) {
+        f_lo[0] = f_hi[0] = f_lo[1] = f_hi[1] = 0;
+        f_val[0] = f_val[1] = 0;
+    }
+    __syncthreads();
+    if (word != ~0ull) {
+        const u64 m = word >> 36;
+        const u32 code = (u32)(word >> 34) & 3u, stf = (u32)(word >> 32) & 3u;
+        const int ret = (int)(u32)word;
+        const u64 pos_m = P + m * g;
+        const u64 slot_m = (u64)nf + m;
+        nf2 = nf + (u32)m;
+        P2 = pos_m;
+        short_passes = first ? 0u : sd->short_passes;
+        phase = SD_DONE;
+        if (code == 1) {
+            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + pos_m + (u32)ret; f_val[0] = slot_m; }
+            nf2 += 1;
+            P2 = pos_m + (u32)ret;
+            g2 = (u32)ret;
+            if (P2 < len) {                                                  // else: consumed the whole stream
+                phase = SD_PASSES;
+                if (m < 64 && ++short_passes >= 2) phase = SD_WALK;
+            }
+        } else if (code == 2) {                                              // ret <= 0: unmasked, walk ends
+            if (ret != 0) { nf2 += 1; status = WEBSOCKET_SEG_ERR_DECODE; }
+            else extra = 1;
+            // its payload extent: the header at pos_m again (the buffer is not written yet)
+            const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + pos_m);
+            const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+            u64 h0, h1;
+            ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+            const WsHdr h = ws_parse(h0, h1, len - pos_m);
+            const u64 p1 = lead0 + pos_m + h.hdr + (h.masked ? h.plen : 0);
+            if (threadIdx.x == 0) {
+                f_lo[0] = lead0 + pos_m; f_hi[0] = p1; f_val[0] = slot_m;
+                f_lo[1] = p1; f_hi[1] = lead0 + len; f_val[1] = (u64)nf2 + extra;
+            }
+        } else {
+            status = stf == 1 ? WEBSOCKET_SEG_MAX_FRAMES : (stf == 2 ? WEBSOCKET_SEG_ERR_LEN_WRAP : WEBSOCKET_SEG_OK);
+            if (threadIdx.x == 0) { f_lo[0] = lead0 + pos_m; f_hi[0] = lead0 + len; f_val[0] = nf2; }
+        }
+    }
+    __syncthreads();
+    const u64 t0 = (u64)blockIdx.x * SPASS_T + threadIdx.x, ts = (u64)gridDim.x * SPASS_T;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+        for (u64 p = ((f_lo[f] + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + t0; (p << PIECE_SHIFT_S) < f_hi[f] && p < pend;
+             p += ts)
+            ptr[p] = f_val[f];
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&sd->ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        sd->ticket = 0;
+        sd->stop[0] = sd->stop[1] = 0;
+        sd->P = P2;
+        sd->g = g2;
+        sd->nf = nf2;
+        sd->short_passes = short_passes;
+        sd->phase = phase;
+        if (phase == SD_DONE) {
+            sd->extra = extra;
+            sd->status = status;
+            nwork[0] = nf2 + extra;
+            ws_store_res(res, P2 < len ? P2 : len, nf2, status);
+        }
+        if (mirror) {
+            mirror->P = P2;
+            mirror->g = g2;
+            mirror->nf = nf2;
+            mirror->phase = phase;
+            __threadfence_system();
+            __hip_atomic_store(&mirror->gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    // the rest of a stream whose lengths keep changing (or whose rounds ran out): one wavefront
+    if (finish && phase != SD_DONE && threadIdx.x < 64)
+        stream_walk(buf, len, P2, g2, nf2, len, true, max_frames, desc, items, ptr, pend, nwork, res, threadIdx.x);
+}
+
+// Whatever an eager call's rounds left, when the chunk-parallel walk does not apply: one
+// wavefront walks from the state's (P, g, nf) to the end
 __global__ __launch_bounds__(64) void ws_stream_finish_kernel(const unsigned char* __restrict__ buf, u64 len,
                                                               u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
                                                               u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                               u32* __restrict__ nwork,
                                                               WebsocketSegResult_t* __restrict__ res,
-                                                              SdState* __restrict__ sd) {
+                                                              const SdState* __restrict__ sd) {
     if (sd->phase == SD_DONE) return;
     stream_walk(buf, len, sd->P, sd->g, sd->nf, len, true, max_frames, desc, items, ptr, pend, nwork, res, threadIdx.x);
 }
@@ -623,8 +656,14 @@ struct RwScratch {
     void* h = nullptr;
 };
 
+// (the aux head holds the pass loop's state: the walk's scratch starts after it)
 static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch* out) {
-    return ws_aux_workspace(dbytes, hbytes, st, &out->d, &out->h);
+    WsAux A;
+    const int rc = ws_aux_workspace(WS_AUX_HEAD + dbytes, WS_AUX_HEAD + hbytes, st, &A);
+    if (rc) return rc;
+    out->d = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
+    out->h = reinterpret_cast<unsigned char*>(A.h) + WS_AUX_HEAD;
+    return 0;
 }
 
 static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
@@ -810,15 +849,27 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         return ws_set_msg("websocketframeStreamDecodeDevice: d_desc/d_res not 16-B aligned");
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     hipError_t e;
-    // workspace: the piece path's layout for one segment [0, len), then the pass loop's
-    // state and the segment's (offset, length) pair for the unmask kernel
+    // workspace: the piece path's layout for one segment [0, len), then the segment's
+    // (offset, length) pair for the unmask kernel; the pass loop's state rests in the head
+    // of the stream's auxiliary workspace
     const size_t pws = ws_piece_workspace_bytes(len, 1, max_frames);
     void* ws = nullptr;
-    int rc = ws_device_workspace(pws + 256, st, &ws);
+    int rc = ws_device_workspace(pws + 64, st, &ws);
     if (rc) return rc;
     unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
-    SdState* sd = reinterpret_cast<SdState*>(w8 + ((pws + 63) & ~(size_t)63));
-    u64* d_seg = reinterpret_cast<u64*>(reinterpret_cast<unsigned char*>(sd) + 128);   // [0] offset 0, [1] length
+    u64* d_seg = reinterpret_cast<u64*>(w8 + ((pws + 15) & ~(size_t)15));    // [0] offset 0, [1] length
+    const bool capture = ws_capturing(st);
+    // An eager call on a stream long enough for the chunk-parallel walk reads the state after
+    // every round (published by the resolve kernel into pinned host memory, no copy): another
+    // round while rounds pay, the chunk-parallel walk once lengths keep changing. A captured
+    // call (and any shorter stream) never reads it: `nr` rounds, the last one's resolve also
+    // walks whatever is left with one wavefront.
+    const bool host_rw = ws_stream_rw && len >= RW_MIN && !capture;
+    WsAux A;
+    if ((rc = ws_aux_workspace(WS_AUX_HEAD, host_rw ? WS_AUX_HEAD : 0, st, &A))) return rc;
+    SdState* sd = reinterpret_cast<SdState*>(A.d);
+    SdMirror* hm = host_rw ? reinterpret_cast<SdMirror*>(A.h) : nullptr;
+    SdMirror* dm = host_rw ? reinterpret_cast<SdMirror*>(A.h_dev) : nullptr;
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
     L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
@@ -838,57 +889,66 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         b = (b + 4 + 15) & ~(size_t)15;
         Pw.items = reinterpret_cast<u32x4*>(w8 + b);
     }
-    hipLaunchKernelGGL(ws_stream_init_kernel, dim3(1), dim3(1), 0, st, sd, d_seg, (u64)len, Pw.disorder);
-    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_init_kernel launch", e);
+    if (!*A.state_ok) {                       // a previous call stopped between its launches
+        hipLaunchKernelGGL(ws_stream_init_kernel, dim3(1), dim3(1), 0, st, sd);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_init_kernel launch", e);
+    }
+    *A.state_ok = false;
     // pass B's grid: every candidate a stream of this length and max_frames can have, grid-stride
     u64 kmax = std::min<u64>(std::min<u64>(len / 2 + 1, (u64)max_frames + 1), SD_KMAX);
     const u32 b_blocks = (u32)std::max<u64>(1, std::min<u64>((kmax + SPASS_T - 1) / SPASS_T, 8192));
-    auto rounds = [&](int n) -> int {
-        for (int r = 0; r < n; ++r) {
+    int round = 0;
+    auto rounds = [&](int n, bool finish_last, u32 tag) -> int {
+        for (int r = 0; r < n; ++r, ++round) {
+            const int first = round == 0, fin = finish_last && r == n - 1;
             hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(SD_PROBE_K / SPASS_T), dim3(SPASS_T), 0, st, d_buf, (u64)len,
-                               max_frames, 0, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd);
+                               max_frames, 0, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder);
             hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(b_blocks), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
-                               1, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd);
+                               1, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder);
             hipLaunchKernelGGL(ws_stream_resolve_kernel, dim3(64), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
-                               Pw.ptr, Pw.npieces, sd, Pw.nwork, d_res);
+                               first, fin, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, Pw.nwork, d_res, dm, tag);
         }
         const hipError_t e2 = hipGetLastError();
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
     const int nr = ws_stream_rounds >= 1 && ws_stream_rounds <= 64 ? (int)ws_stream_rounds : 4;
-    // A captured call (and any stream too short for the chunk-parallel walk) never reads the
-    // state back: `nr` pass rounds, then the gated one-wavefront walk finishes whatever the
-    // rounds left. An eager call that may need the chunk-parallel walk reads the state after
-    // every round (one small device-to-host copy): another round while they pay, the
-    // chunk-parallel walk once lengths keep changing.
-    const bool host_rw = ws_stream_rw && len >= RW_MIN && !ws_capturing(st);
-    if ((rc = rounds(host_rw ? 1 : nr))) return rc;
-    bool finished = false;
-    if (host_rw) {
-        void* dh = nullptr;
-        void* hh = nullptr;
-        if ((rc = ws_aux_workspace(256, 256, st, &dh, &hh))) return rc;
-        SdState* hs = reinterpret_cast<SdState*>(hh);
-        for (;;) {
-            if ((e = hipMemcpyAsync(hs, sd, sizeof(SdState), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-                (e = hipStreamSynchronize(st)) != hipSuccess)
-                return ws_set_err("stream state D2H", e);
-            if (hs->phase == SD_DONE) { finished = true; break; }
-            if (hs->phase == SD_PASSES) {
-                if ((rc = rounds(1))) return rc;
-                continue;
-            }
-            if (len - hs->P >= RW_MIN) {                                     // lengths keep changing
-                if ((rc = rw_walk(d_buf, len, hs->P, hs->nf, max_frames, d_desc, Pw, d_res, st))) return rc;
-                finished = true;
-            }
-            break;
-        }
+    if (!host_rw) {
+        if ((rc = rounds(nr, true, 0))) return rc;
+        *A.state_ok = true;
+        return ws_launch_piece_unmask(L, Pw, 1, gen);
     }
-    if (!finished) {
-        hipLaunchKernelGGL(ws_stream_finish_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, max_frames, d_desc,
-                           Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, sd);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_finish_kernel launch", e);
+    // eager: one round, then follow the published state
+    auto published = [&](u32 tag) -> int {
+        for (u64 it = 0;; ++it) {
+            if (__atomic_load_n(&hm->gen, __ATOMIC_ACQUIRE) == tag) return 0;
+            if ((it & 1023) == 1023) {
+                const hipError_t q = hipStreamQuery(st);
+                if (q == hipSuccess) {
+                    if (__atomic_load_n(&hm->gen, __ATOMIC_ACQUIRE) == tag) return 0;
+                    return ws_set_msg("websocketframeStreamDecodeDevice: pass state not published");
+                }
+                if (q != hipErrorNotReady) return ws_set_err("stream state wait", q);
+            }
+            __builtin_ia32_pause();
+        }
+    };
+    u32 tag = ws_next_gen();
+    if ((rc = rounds(1, false, tag)) || (rc = published(tag))) return rc;
+    while (hm->phase == SD_PASSES) {
+        tag = ws_next_gen();
+        if ((rc = rounds(1, false, tag)) || (rc = published(tag))) return rc;
+    }
+    *A.state_ok = true;
+    if (hm->phase != SD_DONE) {
+        const u64 P = hm->P;
+        const u32 nf = hm->nf;
+        if (len - P >= RW_MIN) {                                             // lengths keep changing
+            if ((rc = rw_walk(d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
+        } else {
+            hipLaunchKernelGGL(ws_stream_finish_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, max_frames, d_desc,
+                               Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, sd);
+            if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_finish_kernel launch", e);
+        }
     }
     return ws_launch_piece_unmask(L, Pw, 1, gen);
 }
