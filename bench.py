@@ -52,6 +52,17 @@ def decode_path(path, wl):
     return 4 if wl.fps <= 64 and wl.nseg >= 1024 and wl.wire_bytes <= wl.nseg * ((17 << 10) - 64) else 3
 
 
+_RESULT_OUT = None
+
+
+def emit(obj):
+    """The bench line: the only thing this process writes to its real stdout (libraries'
+    stdout — e.g. gloo's connection messages — goes to stderr, see main)"""
+    out = _RESULT_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def timed_region(step, steps, world):
     """The bench contract's timed region: barrier + synchronize, exactly `steps` calls of
     `step` back to back on the current stream, synchronize + barrier. HIP events are
@@ -305,7 +316,7 @@ def run_encode(args, dev, world, rank):
         if rank == 0 and world == 1 and not args.no_cpu else None,
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     return mism
 
 
@@ -422,7 +433,7 @@ def run_stream(args, dev, world, rank):
         "cpu_baseline": None,
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     return mism
 
 
@@ -494,7 +505,7 @@ def run_reasm(args, dev, world, rank):
         "cpu_baseline": cpu,
     }
     if rank == 0:
-        print(json.dumps(out_json), flush=True)
+        emit(out_json)
     return mism
 
 
@@ -727,7 +738,7 @@ def run_strong(args, dev, world, rank):
         "cpu_baseline": None,
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     return 0 if out["verified"] else 1
 
 
@@ -786,6 +797,12 @@ def run_inflight(args, wl0, dev, world, rank):
 
 
 def main():
+    # the contract's single JSON line goes to the real stdout; everything else any library
+    # prints to fd 1 (gloo's "Rank k is connected to ..." lines, runtime chatter) to stderr
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -994,7 +1011,7 @@ def main():
                           "GBps_total": round((world - 1) * wl.wire_bytes / dt / 1e9, 1)}
         del recv
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
     if mism:
