@@ -320,6 +320,31 @@ __global__ __launch_bounds__(256) void ws_calib_windows_wc_kernel(gu32x4* __rest
         if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
 }
 
+// mode 83: as 80, plus K2's lookups between the loads and the stores: a scalar load of a
+// per-piece word from the table b, then 16 lanes load a 16-B entry it points at (entries
+// spread over 16 MB like K2's items), consumed before the stores
+__global__ __launch_bounds__(256) void ws_calib_windows_dep_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw,
+                                                                   const u32* __restrict__ tab,
+                                                                   const u32x4* __restrict__ items, u32 key) {
+    const u64 npieces = (n + 1023) / 1024, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u32 lane = threadIdx.x & 63;
+    const u64 i = piece * 1024 + (threadIdx.x >> 6) * 256 + lane;
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+    const u32 k = *reinterpret_cast<const __attribute__((address_space(4))) u32*>(
+        reinterpret_cast<uintptr_t>(tab + (piece & ((1u << 18) - 1))));
+    u32x4 q = {0, 0, 0, 0};
+    if (lane < 16) q = items[(k + lane) & ((1u << 20) - 1)];
+    const u32 z = (q.x ^ q.y ^ q.z ^ q.w) & 0u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i + 64u * u < n) st16<1>(v[u] ^ (key ^ z), a + i + 64u * u);
+}
+
 // modes 73-75: the segment-kernel shape (segfuse / fused reassembly) without frame logic:
 // one 256-thread block per "segment" of `segc` 16-B chunks (cfg5: 1032), segments taken in
 // two windows (ws_win2), in-place XOR. 73: LDS-DMA of the segment (1 KiB slices by every
@@ -531,6 +556,16 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
                                0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
+    }
+    if (mode == 83) {  // `blocks` = number of windows; d_b: >= 18 MB (a zeroed table + items)
+        const u32 W = blocks > 0 ? (u32)blocks : 2u;
+        const u64 np = (n + 1023) / 1024, ppw = (np + W - 1) / W;
+        const u32* tab = reinterpret_cast<const u32*>(d_b);
+        const u32x4* items = reinterpret_cast<const u32x4*>(reinterpret_cast<unsigned char*>(d_b) + (2u << 20));
+        hipLaunchKernelGGL(ws_calib_windows_dep_kernel, dim3((u32)(ppw * W)), dim3(256), 0, st, a, n, W, ppw, tab,
+                           items, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_dep_kernel launch", e);
     }
     if (mode >= 73 && mode <= 75) {  // `blocks` = chunks per segment (<= 1280)
         const u32 segc = blocks > 0 && blocks <= 1280 ? (u32)blocks : 1032u;
