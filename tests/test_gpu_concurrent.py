@@ -117,3 +117,46 @@ def test_more_streams_than_slots(dev):
                 j.check("slot job %d" % i)
             else:                                  # decoded twice: the wire is back
                 assert np.array_equal(j.d[:len(j.wire)].cpu().numpy(), j.wire), i
+
+
+def test_stream_decodes_from_two_threads(dev):
+    """websocketframeStreamDecodeDevice from two host threads on two HIP streams at once:
+    each (stream) has its own workspace, pass-loop state and walk scratch (round 1 shared
+    one scratch per device)"""
+    from test_gpu_stream import long_stream, mix3
+    from util_amd import wsframe as W2
+    wires = [long_stream(np.random.default_rng(700 + i), (1 << 20) + (i << 18), mix3) for i in range(2)]
+    wires.append(wsynth.make_batch(4000, 0, 1500, 0, 710)[0])
+    wires.append(wsynth.make_batch(4000, 0, 1500, 0, 711)[0])
+    jobs = []
+    for w in wires:
+        n = len(w)
+        d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+        src = torch.from_numpy(w).to(dev)
+        desc = torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev)
+        res = torch.zeros(16, dtype=torch.uint8, device=dev)
+        ob = w.copy()
+        od, orr = oracle_segments(ob, [0], [n], 1 << 15)
+        jobs.append(dict(n=n, d=d, src=src, desc=desc, res=res, ob=ob, orr=orr))
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    errors = []
+
+    def worker(t):
+        try:
+            with torch.cuda.stream(streams[t]):
+                for rep in range(3):
+                    for j in jobs[t::2]:
+                        j["d"][:j["n"]].copy_(j["src"])
+                        W2.stream_decode_device(j["d"], j["n"], 1 << 15, j["desc"], j["res"], stream=streams[t])
+                        streams[t].synchronize()
+                        gr = j["res"].cpu().numpy().view(W2.SEGRES_DTYPE)[0]
+                        assert tuple(gr) == tuple(j["orr"][0]), (t, rep)
+                        assert np.array_equal(j["d"][:j["n"]].cpu().numpy(), j["ob"]), (t, rep)
+        except Exception as e:              # surfaced below
+            errors.append(e)
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[0]

@@ -203,3 +203,27 @@ def test_stream_tiny_frames_medium(dev):
     wire = long_stream(np.random.default_rng(30), 2 << 20, lambda g: g.integers(0, 27), masked=1.0)
     r = run(dev, wire, 1 << 17)
     assert int(r["consumed"]) == len(wire)
+
+
+def test_stream_state_survives_mixed_calls(dev):
+    """the pass loop's state rests in the stream's auxiliary workspace between calls: long
+    changing streams (the chunk-parallel walk grows that workspace), short ones (the walk in
+    the last resolve), batch decodes and reassembly on the same stream in between"""
+    from test_gpu_parity import random_stream as rs
+    long_w = long_stream(np.random.default_rng(31), 3 << 20, mix3)
+    uni, *_ = wsynth.make_batch(3000, 0, 2000, 0, 32)
+    short_w, so, sl = rs(np.random.default_rng(33), 200)
+    for wire, mf in ((uni, 4096), (long_w, 1 << 14), (short_w, 4096), (uni, 4096), (long_w, 1 << 14)):
+        run(dev, wire, mf)
+        # a batch decode on the same (default) stream between stream decodes
+        bw, boff, *_ = wsynth.make_batch(64, 0, 3000, 0, 34)
+        n = len(bw)
+        d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+        d[:n] = torch.from_numpy(bw).to(dev)
+        so_t = torch.tensor([0], dtype=torch.int64, device=dev)
+        sl_t = torch.tensor([n], dtype=torch.int64, device=dev)
+        desc = torch.zeros(64 * 32, dtype=torch.uint8, device=dev)
+        res = torch.zeros(16, dtype=torch.uint8, device=dev)
+        W.batch_decode_device(d, so_t, sl_t, 64, desc, res)
+        torch.cuda.synchronize()
+        assert int(res.cpu().numpy().view(W.SEGRES_DTYPE)[0]["n_frames"]) == 64
