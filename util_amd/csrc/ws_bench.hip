@@ -376,21 +376,24 @@ __global__ __launch_bounds__(256) void ws_calib_seg_kernel(gu32x4* __restrict__ 
             if (c < segc) st16<1>(win[c] ^ key, g + c);
         }
     } else {
+        // MODE 84/85: 74/75 with each wave's U loads over consecutive chunks (wave w: chunks
+        // [w*U*64, (w+1)*U*64)), K2's layout
+        auto ci = [&](int u) -> u32 { return (MODE == 84 || MODE == 85) ? wv * (U * 64) + u * 64 + lane : u * 256 + tid; };
         u32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const u32 c = u * 256 + tid;
+            const u32 c = ci(u);
             v[u] = ld16<1>(g + (c < segc ? c : segc - 1));
         }
-        if (MODE == 75) {
+        if (MODE == 75 || MODE == 85) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) win[u * 256 + tid] = v[u];
+            for (int u = 0; u < U; ++u) win[ci(u)] = v[u];
             __syncthreads();
             key ^= win[(tid * 7) & (U * 256 - 1)].x & 0u;   // a dependent LDS read (value unused)
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const u32 c = u * 256 + tid;
+            const u32 c = ci(u);
             if (c < segc) st16<1>(v[u] ^ key, g + c);
         }
     }
@@ -567,7 +570,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_dep_kernel launch", e);
     }
-    if (mode >= 73 && mode <= 75) {  // `blocks` = chunks per segment (<= 1280)
+    if ((mode >= 73 && mode <= 75) || mode == 84 || mode == 85) {  // `blocks` = chunks per segment (<= 1280)
         const u32 segc = blocks > 0 && blocks <= 1280 ? (u32)blocks : 1032u;
         const u64 nseg = n / segc;
         const u32 half = nseg >= 512 ? (u32)((nseg + 1) / 2) : 0u;
@@ -575,6 +578,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         if (mode == 73) hipLaunchKernelGGL((ws_calib_seg_kernel<73, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
         if (mode == 74) hipLaunchKernelGGL((ws_calib_seg_kernel<74, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
         if (mode == 75) hipLaunchKernelGGL((ws_calib_seg_kernel<75, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        if (mode == 84) hipLaunchKernelGGL((ws_calib_seg_kernel<84, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        if (mode == 85) hipLaunchKernelGGL((ws_calib_seg_kernel<85, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_seg_kernel launch", e);
     }
