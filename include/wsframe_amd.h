@@ -205,16 +205,18 @@ WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, un
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
- * configuration): "path" (-1 auto, 0 segment blocks, 1 walker, 2 split, 3 piece,
- * 4 segfuse), "piece_scan", "piece_whole", "segfuse_cfg", "reasm_path" (0 auto,
- * 1 fused, 2 three-kernel), "reasm_cfg", "encode_side", "host_chunk_mb", "dyn"
- * (1 dynamic segment dequeue / 0 static), "unroll" (2|4|8 x 16-B chunks per lane per
- * batch), "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
- * "blocks_per_cu" (0 = resident limit), "piece_win" (log2 of the windows the unmask
- * kernel streams side by side, default 1), "piece_wn" / "piece_wbit" (other window
- * maps), "seg_win" / "scan_win" / "enc_win" (two windows for the segment kernels / the
- * walk / encode), "k2_timing" (see websocketframeGpuGetStat). Returns 0, or -1 for an unknown name. Not
- * thread-safe against concurrent calls. */
+ * configuration; none changes results): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse),
+ * "piece_scan" (walk lanes per segment: 0 one, 1/2/3/4 64/32/16/8), "piece_whole",
+ * "piece_occ", "piece_win" (log2 of the windows the unmask kernel streams side by side,
+ * default 1), "piece_wn" / "piece_wbit" (other window maps), "seg_win" / "scan_win" /
+ * "enc_win" (two windows for the segment kernels / the walk; encode 1 two windows, 2
+ * XCD-contiguous), "seg_lds" (unused LDS per segment block), "segfuse_cfg", "reasm_path"
+ * (0 auto, 1 fused, 2 three-kernel), "reasm_cfg", "reasm_merge", "encode_side",
+ * "encode_fused", "host_chunk_mb", "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw
+ * stream: chunk-parallel walk, its largest chunk, pass rounds of a captured call), "dyn",
+ * "unroll", "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
+ * "blocks_per_cu", "k2_timing" (see websocketframeGpuGetStat). Options are atomics read
+ * once per call. Returns 0, or -1 for an unknown name. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
 /* Counters of the calling process's most recent call (diagnostics): "stream_rw_chunks"
