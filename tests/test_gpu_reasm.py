@@ -283,3 +283,43 @@ def test_reassemble_cache_limit_random_vs_oracle(dev, limit):
     od, orr, _, _, _, _ = oracle_reassemble(wire, so, sl, 16, open0, None, limit, cached0)
     assert (orr["status"] == -4).any(), "the limit never triggered: the case tests nothing"
     check(dev, wire, so, sl, 16, open_in=open0, readcache_max=limit, cached_in=cached0, tag="limit %d" % limit)
+
+
+@pytest.mark.parametrize("limit,overflow", [(16 * 1024, False), (16 * 1024 - 1, True)], ids=["fits", "one_byte_short"])
+def test_reassemble_cfg5_cache_limit_full_size(dev, limit, overflow):
+    """cfg5 at full size (262,144 messages of 16 x 1 KiB) under a fragment-cache limit: a
+    16 KiB limit holds every message (the FIN fragment brings the cache to exactly the limit:
+    no overflow); one byte less refuses every segment's 16th fragment
+    (WEBSOCKET_SEG_ERR_CACHE_OVERFLOW, 15 frames consumed; the open message is reported
+    incomplete, never delivered); a reduced size is compared with the oracle frame for frame"""
+    wl = bench.Workload.make("cfg5", dev)
+    n, nseg = wl.wire_bytes, wl.nseg
+    out = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    desc = torch.empty(nseg * 16 * 32, dtype=torch.uint8, device=dev)
+    msg = torch.empty(nseg * 16 * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(nseg * 16, dtype=torch.uint8, device=dev)
+    nmsg = torch.zeros(nseg, dtype=torch.int32, device=dev)
+    op = torch.zeros(nseg, dtype=torch.uint8, device=dev)
+    ca = torch.zeros(nseg, dtype=torch.int32, device=dev)
+    W.batch_reassemble_device(wl.buf, wl.seg_off, wl.seg_len, 16, desc, res, out, msg, nmsg, open_state=op,
+                              readcache_max=limit, cached=ca)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(W.SEGRES_DTYPE)
+    nm = nmsg.cpu().numpy()
+    cached = ca.cpu().numpy().view(np.uint32)
+    fw = 1024 + 8                                                   # a 1 KiB fragment on the wire
+    if overflow:
+        assert (r["status"] == W.SEG_ERR_CACHE_OVERFLOW).all() and (r["n_frames"] == 16).all()
+        assert (r["consumed"] == 15 * fw).all() and (nm == 1).all()
+        m = msg.cpu().numpy().view(W.MSG_DTYPE).reshape(nseg, 16)[:, 0]
+        assert (m["complete"] == 0).all() and (m["len"] == 15 * 1024).all()
+    else:
+        assert (r["status"] == W.SEG_OK).all() and (r["n_frames"] == 16).all() and (nm == 1).all()
+        assert (r["consumed"] == 16 * fw).all() and (cached == 0).all() and (op.cpu().numpy() == 0).all()
+        m = msg.cpu().numpy().view(W.MSG_DTYPE).reshape(nseg, 16)[:, 0]
+        assert (m["len"] == 16 * 1024).all() and (m["complete"] == 1).all()
+    # frame for frame against the oracle on the first 512 segments
+    k = 512
+    wire = wl.buf[:int(wl.seg_off_h[k])].cpu().numpy().copy()
+    check(dev, wire, wl.seg_off_h[:k], wl.seg_len_h[:k], 16, tag="cfg5 limit", readcache_max=limit,
+          cached_in=[0] * k)
