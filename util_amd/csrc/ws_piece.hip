@@ -17,7 +17,7 @@
 //   marks the batch unordered.
 // K2 ws_piece_unmask_kernel — one 256-thread block per piece, 4 chunks per lane:
 //   payload loads first, then (while they are in flight) the piece pointer and the
-//   items it leads to (64 per load, hopping to the next segment when the piece
+//   items it leads to (16, then 64 per load, hopping to the next segment when the piece
 //   extends past the current one), XOR masks accumulated per chunk, one 16-B store
 //   per fully covered chunk, exact byte stores at payload edges. Every piece is
 //   touched by exactly one block, so no byte is stored twice.
