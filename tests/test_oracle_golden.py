@@ -303,3 +303,41 @@ def test_reference_reactor_with_amd_glue(golden):
         r = X.reactor_deliver(wire, 1500, c["readcache_max"], on_decode=glue)
         v = (r["lens"], R.sha256(r["bodies"]), r["consumed"], r["frames"], r["detach_error"], r["pending"], r["cached"])
         assert v == tuple(_fixture_view(c)), c["name"]
+
+
+def test_reference_reactor_with_batch_glue(golden, tmp_path):
+    """the GPU integration at the plugin seam: a channel's inbuf decoded as a batch (here by
+    the oracle, bit-identical to the GPU's batch decode) is read by the reference's own
+    reactor, whose on_decode replays the batch's descriptors through libwsframe_amd.so's
+    websocketframeOnDecodeBatch — the deliveries (fragment cache, limit, detach included)
+    are the fixture's, i.e. the reference's own websocketframeDecode's. Streams that arrive
+    in one read (the cursor covers one inbuf fill)."""
+    import os
+    import subprocess
+    import reasm_cases as R
+    from oracle_lib import oracle_segments
+    from util_amd import load_lib
+    X = _reference_reactor()
+    lib = load_lib()
+    here = os.path.dirname(os.path.abspath(__file__))
+    so_path = str(tmp_path / "libtramp.so")
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", os.path.join(os.path.dirname(here), "include"),
+                    os.path.join(here, "c", "batch_glue_tramp.c"), "-o", so_path,
+                    "-L", os.path.dirname(lib._name), "-lwsframe_amd", "-Wl,-rpath," + os.path.dirname(lib._name)],
+                   check=True)
+    tr = C.CDLL(so_path)
+    tr.tramp_set.argtypes = [C.c_void_p, C.c_uint, C.c_ulonglong, C.c_int]
+    glue = C.cast(tr.tramp_on_decode, C.c_void_p).value
+    done = 0
+    for c, wire in _reasm_cases(golden):
+        if len(wire) > 64 << 10:
+            continue
+        dec = wire.copy()
+        od, orr = oracle_segments(dec, [0], [len(dec)], 1 << 16)      # the batch decode, in place
+        desc = np.ascontiguousarray(od[:max(1, int(orr[0]["n_frames"]))])
+        tr.tramp_set(desc.ctypes.data, int(orr[0]["n_frames"]), int(orr[0]["consumed"]), int(orr[0]["status"]))
+        r = X.reactor_deliver(dec, len(dec) + 1, c["readcache_max"], on_decode=glue)
+        v = (r["lens"], R.sha256(r["bodies"]), r["consumed"], r["frames"], r["detach_error"], r["pending"], r["cached"])
+        assert v == tuple(_fixture_view(c)), c["name"]
+        done += 1
+    assert done >= 5
