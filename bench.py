@@ -87,9 +87,11 @@ def timed_region(step, steps, world):
     return time.perf_counter() - t0, e0.elapsed_time(e1) / steps
 
 
-def pmc_traffic(kernel, algo_bytes):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this kernel
-    and workload (profiles/<tag>_pmc.json, tools/prof_summary.py), else None."""
+def pmc_traffic(kernel, algo_bytes, metric):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this kernel,
+    workload and bench metric (profiles/<tag>_pmc.json, tools/prof_summary.py), else None.
+    The metric keeps one op's profile from standing in for another op's that runs the same
+    kernel over the same bytes (cfg3 batch decode and cfg3 stream decode both end in K2)."""
     import glob
     best = None
     for f in glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")):
@@ -98,7 +100,7 @@ def pmc_traffic(kernel, algo_bytes):
         except ValueError:
             continue
         if kernel in rec.get("kernel", "") and rec.get("algo_bytes_per_launch") == algo_bytes \
-                and rec.get("traffic_bytes_per_launch"):
+                and rec.get("bench_metric") == metric and rec.get("traffic_bytes_per_launch"):
             if best is None or os.path.getmtime(f) > os.path.getmtime(best[0]):
                 best = (f, rec)
     return best
@@ -293,9 +295,10 @@ def run_encode(args, dev, world, rank):
     mism = int(D.allreduce([wl.verify()], device=dev)[0])
     mean_kern = float(kern_ms.mean()) / 1e3
     achieved = wl.algo_bytes / mean_kern / 1e9
-    pmc = pmc_traffic("ws_enc_copy_kernel", wl.algo_bytes)
+    metric = "WebSocket client encode+mask GiB/s (device-resident), %d x %d B frames" % (wl.nframes, wl.plen)
+    pmc = pmc_traffic("ws_enc_copy_kernel", wl.algo_bytes, metric)
     out = {
-        "metric": "WebSocket client encode+mask GiB/s (device-resident), %d x %d B frames" % (wl.nframes, wl.plen),
+        "metric": metric,
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
@@ -477,12 +480,13 @@ def run_reasm(args, dev, world, rank):
     algo = wl.wire_bytes + wl.payload_bytes
     fused = reasm_fused(wl)
     kname = "ws_reasm_seg_kernel" if fused else "ws_reasm_gather_kernel"
-    pmc = pmc_traffic(kname, algo)
+    metric = "WebSocket fused unmask + message reassembly GiB/s of bodies (device-resident)"
+    pmc = pmc_traffic(kname, algo, metric)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wl.host_sample(262144), args.cpu_threads or None, op="reasm", frames_per_segment=wl.fps)
     out_json = {
-        "metric": "WebSocket fused unmask + message reassembly GiB/s of bodies (device-resident)",
+        "metric": metric,
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
@@ -961,13 +965,14 @@ def main():
     step_kern = float(kern_ms.mean()) / 1e3
     mean_kern = k2_ms / 1e3 if k2_ms else step_kern
     achieved = wl.algo_bytes / step_kern / 1e9                      # the step: the contract's timed region
-    pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes)
+    metric = "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames"
+    pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes, metric)
     timed = ("HIP events at the two ends of the contract's timed region on the calls' stream / steps: " +
              STEP_KERNELS.get(kpath, KERNELS[kpath]))
     kernel_timed = ("HIP events recorded around every ws_piece_unmask_kernel launch on the calls' stream (library "
                     "option k2_timing), a second region of %d calls" % args.steps) if k2_ms else timed
     out = {
-        "metric": "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,

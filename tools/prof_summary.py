@@ -77,6 +77,7 @@ def main():
         "fetch_bytes_corrected": 2 * fetch_kib * 1024 if fetch_kib is not None else None,
         "write_bytes": write_kib * 1024 if write_kib is not None else None,
         "algo_bytes_per_launch": algo,
+        "bench_metric": bench.get("metric"),
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB -> bytes",
     }
     if fetch_kib is not None and write_kib is not None:
@@ -88,6 +89,8 @@ def main():
         rf["traffic"] = int(rec["traffic_bytes_per_launch"])
         rf["traffic_source"] = "profiles/%s_pmc.json" % tag
         rf["traffic_kernels"] = names
+        if "per_kernel_ns_profiled" in rf:
+            rf["per_kernel_ns_profiled"] = rec["per_kernel_avg_ns"]
     json.dump(rec, open(os.path.join(out, tag + "_pmc.json"), "w"), indent=1)
     json.dump(bench, open(os.path.join(out, tag + "_bench.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
