@@ -311,8 +311,8 @@ def run_encode(args, dev, world, rank):
                      "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
                      "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
                      "kernel": "ws_enc_copy_kernel", "algo_bytes_per_launch": wl.algo_bytes,
-                     "timed": "HIP events at the two ends of the timed region on the calls' stream / steps: hipcub scan + ws_enc_ptr_kernel + "
-                              "ws_enc_copy_kernel + ws_enc_edge_kernel",
+                     "timed": "HIP events at the two ends of the timed region on the calls' stream / steps: ws_enc_tsum_kernel + "
+                              "ws_enc_tscan_kernel + ws_enc_front_kernel + ws_enc_copy_kernel",
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
         "cpu_baseline": cpu_encode_baseline(wl, args.cpu_threads or cpu_thread_counts()[-1])

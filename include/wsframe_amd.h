@@ -211,8 +211,9 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * default 1), "piece_wn" / "piece_wbit" (other window maps), "seg_win" / "scan_win" /
  * "enc_win" (two windows for the segment kernels / the walk; encode 1 two windows, 2
  * XCD-contiguous), "seg_lds" (unused LDS per segment block), "segfuse_cfg", "reasm_path"
- * (0 auto, 1 fused, 2 three-kernel), "reasm_cfg", "reasm_merge", "encode_side",
- * "encode_fused", "host_chunk_mb", "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw
+ * (0 auto, 1 fused, 2 three-kernel), "reasm_cfg", "reasm_merge", "enc_front" (encode:
+ * 1 tile-scan front with the edge chunks before the copy, 0 hipcub scan and an edge
+ * kernel after it), "encode_side", "encode_fused", "host_chunk_mb", "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw
  * stream: chunk-parallel walk, its largest chunk, pass rounds of a captured call), "dyn",
  * "unroll", "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
  * "blocks_per_cu", "k2_timing" (see websocketframeGpuGetStat). Options are atomics read

@@ -20,6 +20,15 @@ def dev():
     return torch.device("cuda:0")
 
 
+@pytest.fixture(autouse=True, params=[1, 0], ids=["front", "hipcub"])
+def front(request, dev):
+    """every test runs on both fronts: F1-F3 (tile scan + per-frame offsets, piece pointers
+    and edge chunks before E3) and hipcub scan + E2, E3, E4"""
+    W.set_option("enc_front", request.param)
+    yield request.param
+    W.set_option("enc_front", 1)
+
+
 def random_frames(rng, n, edge=True, max_len=20000):
     choices = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 125, 126, 127, 1023, 4096, 65535, 65536, 70001]
     lens = [int(rng.choice(choices)) if edge and rng.random() < 0.5 else int(rng.integers(0, max_len))
@@ -118,3 +127,28 @@ def test_encode_then_device_decode_roundtrip(dev):
     ob = wire.copy()
     _, orr = oracle_segments(ob, [int(off[c]) for c in cuts], [e - int(off[c]) for c, e in zip(cuts, ends)], 8)
     assert np.array_equal(r, orr)
+
+
+def test_encode_many_tiles(dev):
+    """300 K frames: 1172 tiles of 256 frames, so the one-block tile scan sums two tiles per
+    thread; short payloads mix the shift path (>= 32 B) with the byte path"""
+    rng = np.random.default_rng(13)
+    n = 300000
+    lens = rng.integers(0, 300, n)
+    lens[rng.random(n) < 0.001] = 70000                                  # some 64-bit length headers
+    src = rng.integers(0, 256, int(lens.max()) + 64, dtype=np.uint8)
+    fr = np.zeros(n, W.ENC_DTYPE)
+    fr["src_off"] = rng.integers(0, 64, n)
+    fr["len"] = lens
+    fr["mask_key"] = rng.integers(0, 2**32, n, dtype=np.uint64)
+    fr["type"] = rng.integers(0, 16, n)
+    fr["is_fin"] = rng.integers(0, 2, n)
+    fr["prev_is_fin"] = rng.integers(0, 2, n)
+    fr["masked"] = rng.random(n) < 0.8
+    want, woff = oracle_encode_frames(src, fr)
+    for shift in (0, 5):
+        out, off = gpu_encode(dev, src, fr, dst_shift=shift)
+        assert np.array_equal(off, woff)
+        got = out[shift:shift + len(want)]
+        assert np.array_equal(got, np.frombuffer(want, dtype=np.uint8))
+        assert (out[:shift] == 0xA5).all() and (out[shift + len(want):] == 0xA5).all()

@@ -37,6 +37,7 @@ int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_scan_win;
 extern WsOpt ws_piece_wn;
 extern WsOpt ws_enc_win;
+extern WsOpt ws_enc_front;
 extern WsOpt ws_seg_lds;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_reasm_merge;
@@ -102,6 +103,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
     else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;
     else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
+    else if (!strcmp(name, "enc_front")) ws_enc_front = (int)value;
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = (int)value;
         ws_k2_timing_reset();

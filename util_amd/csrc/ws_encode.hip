@@ -6,17 +6,22 @@
 // which the reference's encoder never sets), followed by the payload XORed with the
 // key. Frames are laid out back to back in d_dst.
 //
-// E1 hipcub exclusive scan of the wire lengths -> d_wire_off[0..n] (n+1: total last).
-// E2 one thread per frame: every 16 KiB output piece whose first byte lies in the
-//    frame's wire range gets the frame index (pieces past the end: none).
+// Default front (enc_front 1), before E3:
+// F1 one thread per frame: wire bytes of each 256-frame tile.
+// F2 one block: exclusive scan of the tile sums; d_wire_off[n] = the total.
+// F3 one thread per frame: its wire offset (tile prefix + block scan) -> d_wire_off[i];
+//    every 16 KiB output piece whose first byte lies in the frame's wire range gets the
+//    frame index (pieces past the end: none); and the frame's edge chunks (E4 below).
 // E3 one-shot 256-thread block per output piece, 4 x 16 B chunks per lane: the wave
 //    reads up to 64 frame records from its piece's first frame, then every chunk that
 //    lies inside one payload is one unaligned 16-B source load + XOR + aligned store.
-// E4 one thread per frame assembles the other chunks whose first byte lies in its wire
-//    extent (header bytes, frame edges; header bytes computed, payload bytes loaded)
-//    and stores each with one 16-B store. Every output chunk is written exactly once.
-//    E4 touches only chunks E3 skips; option "encode_side" runs it on a side stream
-//    concurrently with E2+E3 (measured slower on MI355X, so off by default).
+// E4 (edge chunks) every chunk whose first byte lies in the frame's wire extent and that
+//    is not inside one payload (header bytes, frame edges): frames with >= 32 B payloads
+//    OR byte-shifted header and masked 16-B source windows, the rest assemble byte by
+//    byte; one 16-B store each. Every output chunk is written exactly once.
+// enc_front 0: E1 hipcub exclusive scan -> E2 piece pointers -> E3 -> E4 as its own
+// kernel (after E3, or with "encode_side" on a side stream concurrently with E2+E3 —
+// measured slower on MI355X).
 #include <hipcub/hipcub.hpp>
 
 #include "ws_common.h"
@@ -34,7 +39,8 @@ struct EncFrame {
     u32 b0, masked;
 };
 
-__device__ __forceinline__ EncFrame enc_load(const WebsocketEncodeDesc_t* f, const u64* wire_off, u32 i) {
+// record i with its wire offset `off` (dst-relative)
+__device__ __forceinline__ EncFrame enc_load_at(const WebsocketEncodeDesc_t* f, u32 i, u64 off) {
     const gu32x4* q = gptr<u32x4>(f + i);
     const u32x4 a = q[0];
     const u32 w4 = gptr<u32>(f + i)[4], w5 = gptr<u32>(f + i)[5];
@@ -47,8 +53,12 @@ __device__ __forceinline__ EncFrame enc_load(const WebsocketEncodeDesc_t* f, con
     const u32 op = prev_fin ? type : 0u;                                     // websocketframe.c:176-202
     e.b0 = (fin ? (op | 0x80u) : op) & 0xFFu;
     e.hl = enc_hl(e.len) + (e.masked ? 4u : 0u);
-    e.off = wire_off[i];
+    e.off = off;
     return e;
+}
+
+__device__ __forceinline__ EncFrame enc_load(const WebsocketEncodeDesc_t* f, const u64* wire_off, u32 i) {
+    return enc_load_at(f, i, wire_off[i]);
 }
 
 // byte j of the frame's header (j < hl)
@@ -105,62 +115,117 @@ __device__ __forceinline__ bool enc_edge_eligible(const EncFrame& e, const EncFr
     return !npay || nx.len >= 16;
 }
 
+// 16 bytes as two little-endian words; byte shifts move bytes to higher (shl) or lower
+// (shr) addresses, bytes shifted past either end are dropped
+struct U128 {
+    u64 lo, hi;
+};
+__device__ __forceinline__ U128 u128_of(const u32x4 w) {
+    return {(u64)w.x | ((u64)w.y << 32), (u64)w.z | ((u64)w.w << 32)};
+}
+__device__ __forceinline__ u32x4 u32x4_of(const U128 a) {
+    return (u32x4){(u32)a.lo, (u32)(a.lo >> 32), (u32)a.hi, (u32)(a.hi >> 32)};
+}
+__device__ __forceinline__ U128 u128_shl(const U128 a, u32 nb) {
+    const u32 s = 8u * nb;
+    if (s == 0) return a;
+    if (s >= 128) return {0, 0};
+    if (s < 64) return {a.lo << s, (a.hi << s) | (a.lo >> (64 - s))};
+    return {0, a.lo << (s - 64)};
+}
+__device__ __forceinline__ U128 u128_shr(const U128 a, u32 nb) {
+    const u32 s = 8u * nb;
+    if (s == 0) return a;
+    if (s >= 128) return {0, 0};
+    if (s < 64) return {(a.lo >> s) | (a.hi << (64 - s)), a.hi >> s};
+    return {a.hi >> (s - 64), 0};
+}
+// 16 payload bytes from a source window XORed with the key at phase r (byte t gets key byte (r + t) & 3)
+__device__ __forceinline__ U128 u128_masked(const u32x4 w, u32 key, u32 r) {
+    const u32 k = rotl32(key, (32u - 8u * (r & 3u)) & 31u);
+    const u64 kk = (u64)k | ((u64)k << 32);
+    const U128 a = u128_of(w);
+    return {a.lo ^ kk, a.hi ^ kk};
+}
+// the frame's header (websocketframe.c:176-202 + MASK bit and key) as bytes [0, hl), zero above
+__device__ __forceinline__ U128 enc_header128(const EncFrame& e) {
+    const u32 n = enc_hl(e.len);
+    const u32 b1 = (n == 2 ? (u32)e.len : (n == 4 ? 126u : 127u)) | (e.masked ? 0x80u : 0u);
+    U128 h = {(u64)e.b0 | ((u64)b1 << 8), 0};
+    if (n == 4) h.lo |= (u64)(((u32)e.len >> 8) & 0xFFu) << 16 | (u64)((u32)e.len & 0xFFu) << 24;
+    if (n == 10) {
+        const u64 be = __builtin_bswap64(e.len);                         // big-endian 64-bit length
+        h.lo |= be << 16;
+        h.hi = be >> 48;
+    }
+    if (e.masked) {
+        if (n == 10) h.hi |= (u64)e.key << 16;                           // bytes 10..13
+        else h.lo |= (u64)e.key << (8u * n);                             // bytes 2..5 / 4..7
+    }
+    return h;
+}
+
 // Assemble and store the eligible frame's head / tail chunks that start in [rlo, rhi)
-// (origin-relative): the 16-B source windows they need are loaded together.
+// (origin-relative): the 16-B source windows they need are loaded together, and each
+// chunk is the OR of byte-shifted header and masked-window words (no byte loop).
+// the three 16-B source windows of an edge: the payload's first and last 16 bytes and the next
+// payload's first 16 bytes
+struct EncWin {
+    u32x4 h, t, n;
+};
+__device__ __forceinline__ u32x4 enc_win16(const unsigned char* src, u64 at) {
+    return *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + at));
+}
+
+__device__ __forceinline__ void enc_edge_store_win(gu32x4* base, const EncFrame& e, const EncFrame& nx, bool nxt,
+                                                   u64 lead0, u64 rlo, u64 rhi, const EncWin& W);
+
 __device__ __forceinline__ void enc_edge_store(const unsigned char* __restrict__ src, gu32x4* base,
                                                const EncFrame& e, const EncFrame& nx, bool nxt, u64 lead0,
                                                u64 rlo, u64 rhi) {
     const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
     const u64 X0 = (o + 15) & ~15ull, XT = d1 & ~15ull;
     const bool head = X0 < d0 && X0 >= rlo && X0 < rhi, tail = (d1 & 15) != 0 && XT >= rlo && XT < rhi;
+    const bool npay = tail && nxt && d1 + nx.hl < XT + 16;
+    EncWin W = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    if (head) W.h = enc_win16(src, e.src);
+    if (tail) W.t = enc_win16(src, e.src + e.len - 16);
+    if (npay) W.n = enc_win16(src, nx.src);
+    enc_edge_store_win(base, e, nx, nxt, lead0, rlo, rhi, W);
+}
+
+__device__ __forceinline__ void enc_edge_store_win(gu32x4* base, const EncFrame& e, const EncFrame& nx, bool nxt,
+                                                   u64 lead0, u64 rlo, u64 rhi, const EncWin& W) {
+    const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
+    const u64 X0 = (o + 15) & ~15ull, XT = d1 & ~15ull;
+    const bool head = X0 < d0 && X0 >= rlo && X0 < rhi, tail = (d1 & 15) != 0 && XT >= rlo && XT < rhi;
     const u64 dn0 = d1 + nx.hl;                                          // next payload start
     const bool npay = tail && nxt && dn0 < XT + 16;                      // next payload enters the tail chunk
-    u32x4 wh = {0, 0, 0, 0}, wt = {0, 0, 0, 0}, wn = {0, 0, 0, 0};
-    if (head) wh = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src));
-    if (tail) wt = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + e.src + e.len - 16));
-    if (npay) wn = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + nx.src));
+    const u32x4 wh = W.h, wt = W.t, wn = W.n;
     const u32 kh = e.masked ? e.key : 0u, kn = nx.masked ? nx.key : 0u;
-    if (head) {                                                          // head chunk holds header bytes
-        u32x4 w = {0, 0, 0, 0};
-        for (u32 q = 0; q < 16; ++q) {
-            const u64 y = X0 + q;
-            u32 v;
-            if (y < d0) {
-                v = enc_header_byte(e, (u32)(y - o));
-            } else {
-                const u32 pi = (u32)(y - d0);
-                const u32 wq = pi < 4 ? wh.x : (pi < 8 ? wh.y : (pi < 12 ? wh.z : wh.w));
-                v = ((wq >> (8u * (pi & 3))) ^ (kh >> (8u * (pi & 3)))) & 0xFFu;
-            }
-            put_byte(w, q, v);
-        }
-        base[X0 >> 4] = w;
+    if (head) {                                                          // header bytes from X0, then payload [0, ..)
+        U128 w = u128_shr(enc_header128(e), (u32)(X0 - o));
+        const U128 p = u128_shl(u128_masked(wh, kh, 0), (u32)(d0 - X0));
+        w.lo |= p.lo;
+        w.hi |= p.hi;
+        base[X0 >> 4] = u32x4_of(w);
     }
-    if (tail) {                                                          // tail chunk: this + next frame
-        u32x4 w = {0, 0, 0, 0};
-        u32 cov = 0;
-        for (u32 q = 0; q < 16; ++q) {
-            const u64 y = XT + q;
-            u32 v;
-            if (y < d1) {
-                const u64 pi = y - d0;
-                const u32 t = (u32)(pi - (e.len - 16));
-                const u32 wq = t < 4 ? wt.x : (t < 8 ? wt.y : (t < 12 ? wt.z : wt.w));
-                v = ((wq >> (8u * (t & 3))) ^ (kh >> (8u * (u32)(pi & 3)))) & 0xFFu;
-            } else if (!nxt) {
-                continue;                                                // past the batch
-            } else if (y < dn0) {
-                v = enc_header_byte(nx, (u32)(y - d1));
-            } else {
-                const u32 pi = (u32)(y - dn0);
-                const u32 wq = pi < 4 ? wn.x : (pi < 8 ? wn.y : (pi < 12 ? wn.z : wn.w));
-                v = ((wq >> (8u * (pi & 3))) ^ (kn >> (8u * (pi & 3)))) & 0xFFu;
+    if (tail) {                                                          // payload [len-16, len) then the next frame
+        const u32 r = (u32)(d1 - XT);                                    // payload bytes in the chunk, 1..15
+        U128 w = u128_shr(u128_masked(wt, kh, (u32)e.len), 16u - r);
+        if (nxt) {
+            const U128 h = u128_shl(enc_header128(nx), r);
+            w.lo |= h.lo;
+            w.hi |= h.hi;
+            if (npay) {
+                const U128 p = u128_shl(u128_masked(wn, kn, 0), (u32)(dn0 - XT));
+                w.lo |= p.lo;
+                w.hi |= p.hi;
             }
-            put_byte(w, q, v);
-            cov |= 1u << q;
+            base[XT >> 4] = u32x4_of(w);
+        } else {
+            ws_store_bytes(reinterpret_cast<gu8*>(base + (XT >> 4)), u32x4_of(w), (1u << r) - 1u);   // past the batch
         }
-        if (cov == 0xFFFFu) base[XT >> 4] = w;
-        else ws_store_bytes(reinterpret_cast<gu8*>(base + (XT >> 4)), w, cov);
     }
 }
 
@@ -264,27 +329,21 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
 
 // Every 16-B output chunk that is not inside one payload (header bytes, frame edges,
 // the batch's first and last chunk): assembled by the frame whose wire extent holds the
-// chunk's first byte (frame 0 also takes a chunk starting before the output), byte by
-// byte — header bytes computed, payload bytes loaded — and stored once.
-__global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* __restrict__ src,
-                                                          const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
-                                                          const u64* __restrict__ wire_off,
-                                                          unsigned char* __restrict__ dst, u64 capacity,
-                                                          u32 enc_fused) {
-    const u32 i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+// chunk's first byte (frame 0 also takes a chunk starting before the output) and stored
+// once. Eligible frames (enc_edge_eligible) take the shift path; the rest byte by byte —
+// header bytes computed, payload bytes loaded — walking the following frames with their
+// offsets accumulated from e.off (no wire_off reads past frame i: the front kernel calls
+// this while other blocks are still writing wire_off). skip_eligible: E3 (encode_fused)
+// stores the eligible frames' chunks.
+__device__ __forceinline__ void enc_edges(const unsigned char* __restrict__ src, const WebsocketEncodeDesc_t* __restrict__ f,
+                                          u32 n, u32 i, const EncFrame& e, const EncFrame& nx, unsigned char* dst,
+                                          u64 total, bool skip_eligible) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(dst) & ~(uintptr_t)15);
-    const u64 total = min(wire_off[n], capacity);
     const u64 out_lo = lead0, out_hi = lead0 + total;
-    const EncFrame e = enc_load(f, wire_off, i);
     const u64 o = e.off + lead0, d0 = o + e.hl, d1 = d0 + e.len;
-    // eligible frames: E3 stored their edge chunks (enc_edge_eligible / enc_edge_store)
-    EncFrame nx = {};
-    if (i + 1 < n) nx = enc_load(f, wire_off, i + 1);
-    if (enc_fused && enc_edge_eligible(e, nx, i, n, lead0, out_lo, out_hi)) return;
-    if (!enc_fused && enc_edge_eligible(e, nx, i, n, lead0, out_lo, out_hi)) {
-        enc_edge_store(src, base, e, nx, i + 1 < n, lead0, 0, ~0ull);
+    if (enc_edge_eligible(e, nx, i, n, lead0, out_lo, out_hi)) {
+        if (!skip_eligible) enc_edge_store(src, base, e, nx, i + 1 < n, lead0, 0, ~0ull);
         return;
     }
     u64 X = i ? ((o + 15) & ~15ull) : (o & ~15ull);                           // first chunk start owned
@@ -326,7 +385,7 @@ __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* _
                 put_byte(w, (u32)(y - X), v);
             }
             if (hd1 >= X + 16 || ++g >= n) break;
-            h = enc_load(f, wire_off, g);
+            h = enc_load_at(f, g, h.off + h.hl + h.len);
         }
         gu32x4* const pc = base + (X >> 4);
         if (X >= out_lo && X + 16 <= out_hi) {
@@ -340,6 +399,114 @@ __global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* _
             }
         }
     }
+}
+
+// E4 of the hipcub front (enc_front 0): one thread per frame, offsets from E1's wire_off
+__global__ __launch_bounds__(256) void ws_enc_edge_kernel(const unsigned char* __restrict__ src,
+                                                          const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                          const u64* __restrict__ wire_off,
+                                                          unsigned char* __restrict__ dst, u64 capacity,
+                                                          u32 enc_fused) {
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const u64 total = min(wire_off[n], capacity);
+    EncFrame e = enc_load(f, wire_off, i), nx = {};
+    if (i + 1 < n) nx = enc_load(f, wire_off, i + 1);
+    enc_edges(src, f, n, i, e, nx, dst, total, enc_fused != 0);
+}
+
+// ---- front (enc_front 1): F1 tile sums -> F2 tile scan -> F3 offsets + piece pointers + edges
+// (256-frame tiles; 64-frame tiles, barrier-free, made F2's one-block scan 5 -> 32 us)
+#define ENC_TILE 256
+
+__device__ __forceinline__ u64 enc_wave_incl(u64 v, u32 lane) {
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+        const u64 t = __shfl_up((unsigned long long)v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// F1: wire bytes of each 256-frame tile
+__global__ __launch_bounds__(ENC_TILE) void ws_enc_tsum_kernel(const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                               u64* __restrict__ tsum) {
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32 i = blockIdx.x * ENC_TILE + tid;
+    u64 wl = 0;
+    if (i < n) {
+        const u64 len = f[i].len;
+        wl = (u64)enc_hl(len) + (f[i].masked ? 4u : 0u) + len;
+    }
+    const u64 incl = enc_wave_incl(wl, lane);
+    __shared__ u64 ws[ENC_TILE / 64];
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    if (tid == 0) tsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// F2 (one block): exclusive scan of the B tile sums in place, t[B] = wire_off[n] = total
+__global__ __launch_bounds__(1024) void ws_enc_tscan_kernel(u64* __restrict__ t, u32 B, u64* __restrict__ wire_off,
+                                                            u32 n) {
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32 C = (B + 1023) / 1024, lo = tid * C < B ? tid * C : B, hi = lo + C < B ? lo + C : B;
+    u64 sum = 0;
+    for (u32 j = lo; j < hi; ++j) sum += t[j];
+    const u64 incl = enc_wave_incl(sum, lane);
+    __shared__ u64 ws[16];
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    u64 run = incl - sum;
+    for (u32 w = 0; w < wv; ++w) run += ws[w];
+    const u64 total = run + sum;                                             // thread 1023: the batch total
+    __syncthreads();                                                         // every thread has read its sums
+    for (u32 j = lo; j < hi; ++j) {
+        const u64 v = t[j];
+        t[j] = run;
+        run += v;
+    }
+    if (tid == 1023) {
+        t[B] = total;
+        wire_off[n] = total;
+    }
+}
+
+// F3: one thread per frame — wire offset (tile prefix + block scan), E2's piece pointers,
+// E4's edge chunks
+__global__ __launch_bounds__(ENC_TILE) void ws_enc_front_kernel(const unsigned char* __restrict__ src,
+                                                                const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
+                                                                const u64* __restrict__ tpre, u32 B,
+                                                                u64* __restrict__ wire_off, u32* __restrict__ ptr,
+                                                                u64 npieces, unsigned char* __restrict__ dst,
+                                                                u64 capacity, u32 enc_fused) {
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u32 i = blockIdx.x * ENC_TILE + tid;
+    EncFrame e = {}, nx = {};
+    if (i < n) e = enc_load_at(f, i, 0);
+    if (i + 1 < n) nx = enc_load_at(f, i + 1, 0);
+    const u64 wl = i < n ? e.hl + e.len : 0;
+    const u64 incl = enc_wave_incl(wl, lane);
+    __shared__ u64 ws[ENC_TILE / 64];
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    u64 off = tpre[blockIdx.x] + incl - wl;                                  // tile prefix + block scan
+    for (u32 w = 0; w < wv; ++w) off += ws[w];
+    if (i >= n) return;
+    const u64 all = tpre[B];
+    wire_off[i] = off;
+    e.off = off;
+    nx.off = off + wl;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
+    // piece pointers (ws_enc_ptr_kernel): pieces whose first byte lies in this frame's wire
+    // range get i (frame 0 also owns the origin); the last frame also marks the pieces past the end
+    const u64 a = i ? off + lead0 : 0, b = off + wl + lead0;
+    for (u64 p = (a + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT; (p << ENC_SHIFT) < b && p < npieces; ++p) ptr[p] = i;
+    if (i == n - 1)
+        for (u64 p = (b + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT; p < npieces; ++p) ptr[p] = ENC_NONE;
+    // the edge windows are loaded once the offsets say which are needed: loading all three
+    // up front (in flight during the scan) measured 61 -> 92 us on cfg2, the random
+    // source lines being this kernel's bound (profiles/r02_encode_front_ab.log)
+    enc_edges(src, f, n, i, e, nx, dst, min(all, capacity), enc_fused != 0);
 }
 
 int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out);
@@ -370,6 +537,8 @@ WsOpt ws_encode_fused{0}; // "encode_fused": 1 E3 stores the edge chunks of elig
                           // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
 WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (1, ws_win2; measured 1 % slower)
                           // or XCD-contiguous (2)
+WsOpt ws_enc_front{1};    // "enc_front": 1 F1-F3 front (tile sums, tile scan, one thread per frame: offsets,
+                          // piece pointers, edge chunks) before E3; 0 hipcub scan + E2, E3, then E4
 WsOpt ws_encode_side{0};  // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
                           // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
@@ -384,34 +553,53 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     const u64 lead0 = reinterpret_cast<uintptr_t>(d_dst) & 15;
     const u64 npieces = (dst_capacity + lead0 + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT;
-    WireLen op{d_frames, nframes};
-    hipcub::CountingInputIterator<u32> cnt(0);
-    hipcub::TransformInputIterator<u64, WireLen, hipcub::CountingInputIterator<u32>> in(cnt, op);
-    size_t scan_bytes = 0;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, d_wire_off, nframes + 1, st);
-    if (e != hipSuccess) return ws_set_err("hipcub scan (size)", e);
-    const size_t ptr_off = (scan_bytes + 255) & ~(size_t)255;
+    const bool side = ws_encode_side, front = ws_enc_front && !side;
+    const u32 fused = ws_encode_fused && npieces ? 1u : 0u;
+    hipError_t e;
+    int rc;
     void* ws = nullptr;
-    int rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws);
-    if (rc) return rc;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(ws, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
-        return ws_set_err("hipcub scan", e);
-    u32* ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
+    u32* ptr = nullptr;
     EncSide* S = nullptr;
-    if (ws_encode_side) {
-        if ((rc = enc_side(&S))) return rc;
-        if ((e = hipEventRecord(S->fork, st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
-        if ((e = hipStreamWaitEvent(S->s, S->fork, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
-        hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, S->s, d_src, d_frames,
-                           nframes, d_wire_off, d_dst, (u64)dst_capacity, 0u);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
-        if ((e = hipEventRecord(S->join, S->s)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+    if (front) {
+        // F1 tile sums -> F2 tile scan (also wire_off[n]) -> F3 offsets, piece pointers, edges
+        const u32 B = (nframes + ENC_TILE - 1) / ENC_TILE, blocks = B;
+        const size_t ptr_off = ((size_t)(B + 1) * 8 + 255) & ~(size_t)255;
+        if ((rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws))) return rc;
+        u64* tpre = reinterpret_cast<u64*>(ws);
+        ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
+        hipLaunchKernelGGL(ws_enc_tsum_kernel, dim3(blocks), dim3(ENC_TILE), 0, st, d_frames, nframes, tpre);
+        hipLaunchKernelGGL(ws_enc_tscan_kernel, dim3(1), dim3(1024), 0, st, tpre, B, (u64*)d_wire_off, nframes);
+        hipLaunchKernelGGL(ws_enc_front_kernel, dim3(blocks), dim3(ENC_TILE), 0, st, d_src, d_frames, nframes, tpre, B,
+                           (u64*)d_wire_off, ptr, npieces, d_dst, (u64)dst_capacity, fused);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("encode front launch", e);
+    } else {
+        // E1 hipcub scan -> E2 piece pointers (E4 after E3, or on a side stream)
+        WireLen op{d_frames, nframes};
+        hipcub::CountingInputIterator<u32> cnt(0);
+        hipcub::TransformInputIterator<u64, WireLen, hipcub::CountingInputIterator<u32>> in(cnt, op);
+        size_t scan_bytes = 0;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
+            return ws_set_err("hipcub scan (size)", e);
+        const size_t ptr_off = (scan_bytes + 255) & ~(size_t)255;
+        if ((rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws))) return rc;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(ws, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
+            return ws_set_err("hipcub scan", e);
+        ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
+        if (side) {
+            if ((rc = enc_side(&S))) return rc;
+            if ((e = hipEventRecord(S->fork, st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+            if ((e = hipStreamWaitEvent(S->s, S->fork, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
+            hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, S->s, d_src, d_frames,
+                               nframes, d_wire_off, d_dst, (u64)dst_capacity, 0u);
+            if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
+            if ((e = hipEventRecord(S->join, S->s)) != hipSuccess) return ws_set_err("hipEventRecord", e);
+        }
+        hipLaunchKernelGGL(ws_enc_ptr_kernel, dim3((nframes + 1 + 255) / 256), dim3(256), 0, st, d_frames, nframes,
+                           d_wire_off, ptr, lead0, npieces);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     }
-    hipLaunchKernelGGL(ws_enc_ptr_kernel, dim3((nframes + 1 + 255) / 256), dim3(256), 0, st, d_frames, nframes,
-                       d_wire_off, ptr, lead0, npieces);
-    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     if (npieces) {
-        auto copy = ws_encode_fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
+        auto copy = fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
         const int win = ws_enc_win;
         const u32 half = win == 2 ? ~0u : (win == 1 && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0);
         const u32 grid = win == 2 ? (u32)(((npieces + 7) >> 3) << 3) : (half ? 2 * half : (u32)npieces);
@@ -423,8 +611,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         if ((e = hipStreamWaitEvent(st, S->join, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
         return 0;
     }
+    if (front) return 0;
     hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, d_src, d_frames, nframes,
-                       d_wire_off, d_dst, (u64)dst_capacity, (u32)(ws_encode_fused && npieces));
+                       d_wire_off, d_dst, (u64)dst_capacity, fused);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
     return 0;
 }
