@@ -1,0 +1,16 @@
+# A/B of two builds of libwsframe_amd.so (util_amd/libwsframe_amd_base.so vs the current one),
+# interleaved, on one box: bash tools/ab_lib.sh <tag> "<bench args>|<bench args>|..." [rounds]
+set -o pipefail
+tag=$1; IFS='|' read -ra CASES <<< "$2"; rounds=${3:-3}
+mkdir -p gpurun_out
+for r in $(seq 1 $rounds); do
+  for lib in base new; do
+    for c in "${CASES[@]}"; do
+      if [ $lib = base ]; then export WSFRAME_AMD_LIB=$PWD/util_amd/libwsframe_amd_base.so; else unset WSFRAME_AMD_LIB; fi
+      timeout -k 10 180 python bench.py $c --no-cpu --no-e2e --no-xor-stream > gpurun_out/ab_one.json 2>/dev/null || { echo "FAIL $lib $c"; exit 1; }
+      python -c "
+import json,sys;d=json.load(open('gpurun_out/ab_one.json'));r=d['roofline']
+print('$lib', '$c'.strip(), d['ms_per_step'], r['frac'], r.get('kernel_ms_mean'), d['verified'])" | tee -a gpurun_out/ab_$tag.log
+    done
+  done
+done

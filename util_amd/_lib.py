@@ -8,7 +8,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libwsframe_amd.so")
+# (WSFRAME_AMD_LIB: another build of the same library, for A/B measurements only)
+LIB_PATH = os.environ.get("WSFRAME_AMD_LIB") or os.path.join(HERE, "libwsframe_amd.so")
 # bench / test support (synthetic batches generated in HBM, calibration): NOT the drop-in
 BENCH_LIB_PATH = os.path.join(HERE, "libwsframe_amd_bench.so")
 _lib = None

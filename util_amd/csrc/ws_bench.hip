@@ -399,6 +399,57 @@ __global__ __launch_bounds__(256) void ws_calib_seg_kernel(gu32x4* __restrict__ 
     }
 }
 
+// modes 86/87: the segment-kernel shape with every wave owning whole ABSOLUTE 4 KiB pages
+// (the layout of mode 76, which streams 3.3 % faster than 1 KiB rows, kept when blocks are
+// segments at any offset): the segment's chunks [c0, c1) touch pages c0>>8 .. (c1-1)>>8;
+// wave w takes pages w, w+4 of that list. 86: in registers (4 loads per page); 87: LDS-DMA
+// of the page's four 1 KiB rows into a window laid out on the absolute 1 KiB grid, barrier,
+// XOR from LDS and store (segfuse's data path).
+template <int MODE>
+__global__ __launch_bounds__(256) void ws_calib_seg_pages_kernel(gu32x4* __restrict__ a, u64 nseg, u32 segc, u32 half,
+                                                                 u32 key) {
+    __shared__ __attribute__((aligned(16))) u32x4 win[MODE == 87 ? 6 * 256 : 1];
+    const u32 b = half ? (blockIdx.x & 1u) * half + (blockIdx.x >> 1) : blockIdx.x;
+    if (b >= nseg) return;
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u64 c0 = (u64)b * segc, c1 = c0 + segc;
+    const u64 pg0 = c0 >> 8, npg = ((c1 - 1) >> 8) - pg0 + 1;                 // <= 6 pages
+    if (MODE == 86) {
+        for (u64 p = wv; p < npg; p += 4) {
+            u32x4 v[4];
+            const u64 cb = (pg0 + p) << 8;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u64 c = cb + u * 64 + lane;
+                v[u] = ld16<1>(a + (c < c0 ? c0 : (c < c1 ? c : c1 - 1)));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u64 c = cb + u * 64 + lane;
+                if (c >= c0 && c < c1) st16<1>(v[u] ^ key, a + c);
+            }
+        }
+    } else {
+        const u64 wbase = pg0 << 8;                                            // window chunk 0
+        for (u64 p = wv; p < npg; p += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u64 c = ((pg0 + p) << 8) + u * 64 + lane;
+                __builtin_amdgcn_global_load_lds(
+                    reinterpret_cast<const WS_GLOBAL void*>(a + (c < c0 ? c0 : (c < c1 ? c : c1 - 1))),
+                    (ws_lds_void*)(&win[(p << 8) + u * 64]), 16, 0, 2);
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (u64 p = wv; p < npg; p += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u64 c = ((pg0 + p) << 8) + u * 64 + lane;
+                if (c >= c0 && c < c1) st16<1>(win[c - wbase] ^ key, a + c);
+            }
+    }
+}
+
 // mode 16+: one-shot in-place XOR through buffer instructions with explicit cache
 // bits (aux: bit0 sc0, bit1 nt, bit4 sc1), T threads x U chunks per block.
 template <int T, int U, int LAUX, int SAUX>
@@ -582,6 +633,16 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         if (mode == 85) hipLaunchKernelGGL((ws_calib_seg_kernel<85, 5>), dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_seg_kernel launch", e);
+    }
+    if (mode == 86 || mode == 87) {  // `blocks` = chunks per segment (<= 1280: <= 6 pages)
+        const u32 segc = blocks > 0 && blocks <= 1280 ? (u32)blocks : 1032u;
+        const u64 nseg = n / segc;
+        const u32 half = nseg >= 512 ? (u32)((nseg + 1) / 2) : 0u;
+        const u32 grid = half ? 2 * half : (u32)nseg;
+        if (mode == 86) hipLaunchKernelGGL(ws_calib_seg_pages_kernel<86>, dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL(ws_calib_seg_pages_kernel<87>, dim3(grid), dim3(256), 0, st, a, nseg, segc, half, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_seg_pages_kernel launch", e);
     }
     if (mode == 70 || mode == 71) {  // persistent; d_b's first 4 bytes are the ticket counter
         const u32 nb = blocks > 0 ? (u32)blocks : 2048u;

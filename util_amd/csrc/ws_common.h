@@ -145,9 +145,30 @@ __device__ __forceinline__ void ws_store_bytes(WS_GLOBAL unsigned char* p, const
     }
 }
 
+// nibble n (n < 16) -> byte mask (bit i -> 0xFF in byte i): the multiply spreads bit i to
+// bit 8i (the four shifted copies of n do not overlap), giving v_perm_b32 selector bytes
+// 0x0C (-> 0x00) or 0x0D (-> 0xFF)
 __device__ __forceinline__ u32 nib_to_bytemask(u32 n) {
-    return ((n & 1u) ? 0x000000FFu : 0u) | ((n & 2u) ? 0x0000FF00u : 0u) | ((n & 4u) ? 0x00FF0000u : 0u) |
-           ((n & 8u) ? 0xFF000000u : 0u);
+    const u32 sel = ((n * 0x00204081u) & 0x01010101u) | 0x0C0C0C0Cu;
+    return __builtin_amdgcn_perm(0u, 0u, sel);
+}
+
+// OR the XOR masks of the bytes [lo, hi) of a 16-B chunk (0 <= lo < hi <= 16) under `key`
+// (rotated to the chunk's phase: chunk byte i takes key byte i & 3) into m0..m3, and their
+// byte bits into cov. A chunk wholly inside the range — all but the frame-edge chunks —
+// takes four ORs; the byte-mask build runs only when some lane of the wave has an edge.
+__device__ __forceinline__ void ws_or_masks(u32 key, int lo, int hi, u32& m0, u32& m1, u32& m2, u32& m3, u32& cov) {
+    if ((lo | (16 - hi)) == 0) {
+        m0 |= key; m1 |= key; m2 |= key; m3 |= key;
+        cov = 0xFFFFu;
+        return;
+    }
+    const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+    cov |= bits;
+    m0 |= key & nib_to_bytemask(bits & 15u);
+    m1 |= key & nib_to_bytemask((bits >> 4) & 15u);
+    m2 |= key & nib_to_bytemask((bits >> 8) & 15u);
+    m3 |= key & nib_to_bytemask(bits >> 12);
 }
 
 
@@ -163,12 +184,7 @@ __device__ __forceinline__ void ws_store_partial(const u32x4 v, gu32x4* const pc
         if (t.p0 >= x + 16) break;
         const int lo = t.p0 > x ? t.p0 - x : 0, hi = t.p1 < x + 16 ? t.p1 - x : 16;
         if (hi <= lo) continue;
-        const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
-        cov |= bits;
-        m0 |= t.rkey & nib_to_bytemask(bits & 15u);
-        m1 |= t.rkey & nib_to_bytemask((bits >> 4) & 15u);
-        m2 |= t.rkey & nib_to_bytemask((bits >> 8) & 15u);
-        m3 |= t.rkey & nib_to_bytemask(bits >> 12);
+        ws_or_masks(t.rkey, lo, hi, m0, m1, m2, m3, cov);
     }
     u32x4 mm;
     mm.x = m0; mm.y = m1; mm.z = m2; mm.w = m3;

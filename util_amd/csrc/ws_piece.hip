@@ -326,12 +326,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                     const int x = u * 1024 + xl;
                     const int lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
                     if (hi <= lo) continue;
-                    const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
-                    cov[u] |= bits;
-                    m[u][0] |= key & nib_to_bytemask(bits & 15u);
-                    m[u][1] |= key & nib_to_bytemask((bits >> 4) & 15u);
-                    m[u][2] |= key & nib_to_bytemask((bits >> 8) & 15u);
-                    m[u][3] |= key & nib_to_bytemask(bits >> 12);
+                    ws_or_masks(key, lo, hi, m[u][0], m[u][1], m[u][2], m[u][3], cov[u]);
                 }
             }
             if (nlim < step) break;                                         // reached an item past the range

@@ -136,12 +136,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
                 const u32 key = (u32)__builtin_amdgcn_readlane((int)f.rkey, i);
                 const int lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
                 if (hi <= lo) continue;
-                const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
-                cov |= bits;
-                m0 |= key & nib_to_bytemask(bits & 15u);
-                m1 |= key & nib_to_bytemask((bits >> 4) & 15u);
-                m2 |= key & nib_to_bytemask((bits >> 8) & 15u);
-                m3 |= key & nib_to_bytemask(bits >> 12);
+                ws_or_masks(key, lo, hi, m0, m1, m2, m3, cov);
             }
             if (!cov) continue;
             u32x4 w = win[cb + lane];
