@@ -277,6 +277,27 @@ struct BodyL {           // body table entry (LDS; its key, rotated to the absol
     u64 len;             // first body byte region-relative, body length
 };
 
+// Interior copy of one body from the LDS window: output chunks c = lane, lane + 64, ... < nch
+// at dst + 16c take the 16 source bytes at window byte o0 + 16c, XOR key. The source phase
+// o0 & 15 is the same for every chunk of the body (wave-uniform), so the 16 bytes are four
+// v_alignbyte_b32 of dwords picked at compile time (SD = (o0 >> 2) & 3, one loop per SD),
+// not a per-lane 64-bit funnel shift.
+template <int SD>
+__device__ __forceinline__ void reasm_copy(const u32x4* win, u32 o0, u32 nch, u32 key, u64 dst, u32 lane) {
+    const u32 sb = o0 & 3u;
+    for (u32 c = lane; c < nch; c += 64) {
+        const u32 i = (o0 >> 4) + c;
+        const u32x4 a = win[i], b = win[i + 1];
+        const u32 d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        u32x4 w;
+        w.x = __builtin_amdgcn_alignbyte(d[SD + 1], d[SD + 0], sb) ^ key;
+        w.y = __builtin_amdgcn_alignbyte(d[SD + 2], d[SD + 1], sb) ^ key;
+        w.z = __builtin_amdgcn_alignbyte(d[SD + 3], d[SD + 2], sb) ^ key;
+        w.w = __builtin_amdgcn_alignbyte(d[SD + 4], d[SD + 3], sb) ^ key;
+        st16<1>(w, reinterpret_cast<gu32x4*>(dst + ((u64)c << 4)));
+    }
+}
+
 template <int RSEG_L, int MINW>
 __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void ws_reasm_seg_kernel(
     const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
@@ -455,14 +476,11 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
             if (A < B) {
                 const u32 nch = (u32)((B - A) >> 4);
                 const u32 o0 = (u32)(xa - W0 + (A - da));
-                for (u32 c = lane; c < nch; c += 64) {
-                    const u32 o = o0 + (c << 4);
-                    u64 h0, h1;
-                    ws_hdr_from32(win[o >> 4], win[(o >> 4) + 1], o & 15u, h0, h1);
-                    u32x4 w;
-                    w.x = (u32)h0 ^ key; w.y = (u32)(h0 >> 32) ^ key;
-                    w.z = (u32)h1 ^ key; w.w = (u32)(h1 >> 32) ^ key;
-                    st16<1>(w, reinterpret_cast<gu32x4*>(A + ((u64)c << 4)));
+                switch ((o0 >> 2) & 3u) {
+                    case 0: reasm_copy<0>(win, o0, nch, key, A, lane); break;
+                    case 1: reasm_copy<1>(win, o0, nch, key, A, lane); break;
+                    case 2: reasm_copy<2>(win, o0, nch, key, A, lane); break;
+                    default: reasm_copy<3>(win, o0, nch, key, A, lane);
                 }
             }
             const bool mh = (mg >> bi) & 1ull, mt = bi < 63 && ((mg >> (bi + 1)) & 1ull);
