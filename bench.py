@@ -880,9 +880,8 @@ def main():
     # of the wire in one-shot 256 x 4 blocks over 16 KiB pieces in the same two windows, no
     # frame logic (calibration kernel, libwsframe_amd_bench.so mode 72) — how close the decode
     # step is to moving the same bytes with nothing else to do; an even number of calls leaves
-    # the buffer as it was. Measured before the decode's warm-up (>= 100 calls), so a short
-    # timed region (the driver's 20 steps after 5 warm-up calls) starts on a GPU that has been
-    # streaming, as it would in service
+    # the buffer as it was. (Measured before the decode's warm-up; it does not warm the device
+    # up for the decode — tools/exp_ramp.py, DESIGN §4 "Short timed regions".)
     xor_stream = None
     if not args.no_xor_stream:
         lib = wl.W.load_bench_lib()

@@ -25,6 +25,7 @@ extern WsOpt ws_piece_scan;
 extern WsOpt ws_reasm_path;
 extern WsOpt ws_reasm_cfg;
 extern WsOpt ws_segfuse_cfg;
+extern WsOpt ws_enc_lds;
 extern WsOpt ws_encode_side;
 extern WsOpt ws_encode_fused;
 extern WsOpt ws_piece_whole;
@@ -103,6 +104,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
     else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;
     else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
+    else if (!strcmp(name, "enc_lds")) ws_enc_lds = (int)value;
     else if (!strcmp(name, "enc_front")) ws_enc_front = (int)value;
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = (int)value;

@@ -535,6 +535,7 @@ static int enc_side(EncSide** out) {
 }
 WsOpt ws_encode_fused{0}; // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
                           // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
+WsOpt ws_enc_lds{0};      // "enc_lds": bytes of unused dynamic LDS per E3 block (occupancy A/B)
 WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (1, ws_win2; measured 1 % slower)
                           // or XCD-contiguous (2)
 WsOpt ws_enc_front{1};    // "enc_front": 1 F1-F3 front (tile sums, tile scan, one thread per frame: offsets,
@@ -603,7 +604,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         const int win = ws_enc_win;
         const u32 half = win == 2 ? ~0u : (win == 1 && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0);
         const u32 grid = win == 2 ? (u32)(((npieces + 7) >> 3) << 3) : (half ? 2 * half : (u32)npieces);
-        hipLaunchKernelGGL(copy, dim3(grid), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
+        const int dyn = ws_enc_lds;                                            // unused LDS: fewer blocks per CU
+        hipLaunchKernelGGL(copy, dim3(grid), dim3(ENC_T), dyn > 0 && dyn <= 65536 ? dyn : 0, st, d_src, d_frames, nframes,
                            d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, half);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
