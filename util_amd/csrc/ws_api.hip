@@ -30,6 +30,7 @@ extern WsOpt ws_encode_side;
 extern WsOpt ws_encode_fused;
 extern WsOpt ws_piece_whole;
 extern WsOpt ws_piece_occ;
+extern WsOpt ws_piece_lds;
 extern WsOpt ws_piece_win;
 extern WsOpt ws_piece_wbit;
 extern WsOpt ws_k2_timing;
@@ -97,6 +98,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "encode_fused")) ws_encode_fused = (int)value;
     else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
     else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
+    else if (!strcmp(name, "piece_lds")) ws_piece_lds = (int)value;
     else if (!strcmp(name, "piece_win")) ws_piece_win = (int)value;
     else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
     else if (!strcmp(name, "seg_lds")) ws_seg_lds = (int)value;

@@ -172,6 +172,24 @@ __device__ __forceinline__ void ws_or_masks(u32 key, int lo, int hi, u32& m0, u3
 }
 
 
+// As ws_or_masks, XOR-ing straight into the chunk's data (the ranges of different frames
+// never share a byte, so applying each frame's masks at once equals OR-ing them first):
+// no mask registers. The data must be loaded — a wave that waits for its frame records
+// (loaded after its payload) has its payload back anyway (vmcnt retires in order).
+__device__ __forceinline__ void ws_xor_range(u32 key, int lo, int hi, u32x4& v, u32& cov) {
+    if ((lo | (16 - hi)) == 0) {
+        v.x ^= key; v.y ^= key; v.z ^= key; v.w ^= key;
+        cov = 0xFFFFu;
+        return;
+    }
+    const u32 bits = (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
+    cov |= bits;
+    v.x ^= key & nib_to_bytemask(bits & 15u);
+    v.y ^= key & nib_to_bytemask((bits >> 4) & 15u);
+    v.z ^= key & nib_to_bytemask((bits >> 8) & 15u);
+    v.w ^= key & nib_to_bytemask(bits >> 12);
+}
+
 // Chunk at round offset x straddles payload edges: OR the byte ranges of every
 // table item from j on that touches it, XOR, and store exactly those bytes (one
 // 16-B store if the chunk turns out fully covered).

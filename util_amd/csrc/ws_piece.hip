@@ -262,10 +262,9 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
         reinterpret_cast<uintptr_t>(ptr + pidx));
     const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
-    u32 m[PIECE_U][4];
     u32 cov[PIECE_U];
 #pragma unroll
-    for (int u = 0; u < PIECE_U; ++u) { m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0; cov[u] = 0; }
+    for (int u = 0; u < PIECE_U; ++u) cov[u] = 0;
     // no early return: an exit branch here would be hoisted above the payload loads
     u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv, step = 16;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
@@ -326,7 +325,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                     const int x = u * 1024 + xl;
                     const int lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
                     if (hi <= lo) continue;
-                    ws_or_masks(key, lo, hi, m[u][0], m[u][1], m[u][2], m[u][3], cov[u]);
+                    ws_xor_range(key, lo, hi, v[u], cov[u]);                    // unmask in registers
                 }
             }
             if (nlim < step) break;                                         // reached an item past the range
@@ -337,13 +336,13 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
         k = 0;
         step = 16;
     }
-    // ---- 3. store: full chunks one 16-B store, edge chunks exactly the covered bytes
+    // ---- 3. store (v[] holds the unmasked bytes): full chunks one 16-B store, edge chunks
+    //         exactly the covered bytes
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) {
         const u64 c = wc0 + (u64)(u * 64 + lane);
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
-        u32x4 w = v[u];
-        w.x ^= m[u][0]; w.y ^= m[u][1]; w.z ^= m[u][2]; w.w ^= m[u][3];
+        const u32x4 w = v[u];
         if (cov[u] == 0xFFFFu || (WHOLE == 1 && ((whole >> u) & 1u)) || (WHOLE == 2 && segcov[u] == 0xFFFFu)) {
             st16<NT>(w, base + c);
         } else {
@@ -418,6 +417,11 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 // K2 alone over the pieces of a scanned batch
 WsOpt ws_piece_whole{2}; // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
                           // one segment, 0 exact bytes only
+// "piece_lds": bytes of unused dynamic LDS per K2 block, which caps K2's blocks (= waves per
+// SIMD) per CU at 160 KiB / bytes: 30000 -> 5. K2 needs only 58 VGPRs (8 waves/SIMD would
+// fit) but streams best at 5: cfg2 1.363-1.366 ms at 5 against 1.378-1.382 (6), 1.395-1.399
+// (7), 1.402-1.420 (8), 1.386-1.387 (4); cfg3 and cfg4 the same way (profiles/r02_k2_occupancy_ab.log)
+WsOpt ws_piece_lds{30000};
 WsOpt ws_piece_occ{0};   // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
 WsOpt ws_piece_wn{0};    // "piece_wn": >= 2 windows of any count (overrides piece_win/piece_wbit)
 WsOpt ws_piece_wbit{0};  // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
@@ -486,7 +490,8 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen)
     const u64 ppw = wn ? (P.npieces + wn - 1) / wn
                        : (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
     const u64 grid = wn ? ppw * wn : ppw << wshift;
-    hipLaunchKernelGGL(k, dim3((u32)grid), dim3(PIECE_T), 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
+    const int dyn = ws_piece_lds;                                            // unused LDS: fewer blocks per CU
+    hipLaunchKernelGGL(k, dim3((u32)grid), dim3(PIECE_T), dyn > 0 && dyn <= 65536 ? dyn : 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
                        L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
                        L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces, wn);
     const hipError_t e = hipGetLastError();

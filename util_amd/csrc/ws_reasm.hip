@@ -538,9 +538,11 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
 
 // 0 auto, 1 fused segment kernel, 2 scan + layout + gather ("reasm_path")
 WsOpt ws_reasm_path{0};
-// fused kernel geometry ("reasm_cfg"): 0 17 KiB windows + 8 waves/SIMD (SGPR spills: slower),
-// 1 17 KiB windows at the compiler's occupancy (7 waves/SIMD, default), 2 19 KiB windows
-WsOpt ws_reasm_cfg{1};
+// fused kernel geometry ("reasm_cfg"): 0 17 KiB windows + 8 waves/SIMD (default: 49 SGPRs spill
+// to VGPR lanes, yet 1.404-1.411 vs 1.459-1.462 ms on cfg5 once the body copy is alignbyte-based;
+// round 1 measured it slower with the funnel-shift copy), 1 17 KiB windows at the compiler's
+// occupancy (7 waves/SIMD), 2 19 KiB windows
+WsOpt ws_reasm_cfg{0};
 WsOpt ws_reasm_merge{0}; // "reasm_merge": 1 body-boundary chunks assembled whole by one lane, 0 one
                           // byte-store instruction from 31 lanes (default: measured faster, cfg5u 1.50 vs 1.65 ms)
 
