@@ -320,6 +320,23 @@ __global__ __launch_bounds__(256) void ws_calib_windows_wc_kernel(gu32x4* __rest
         if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
 }
 
+// mode 88: as 76 with U chunks per lane (wave w of a 256-thread block covers U KiB of
+// consecutive chunks, a block 4U KiB), two windows, and `dyn` bytes of unused dynamic LDS
+// per block (caps blocks per CU): the shape/occupancy grid for K2
+template <int U>
+__global__ __launch_bounds__(256) void ws_calib_wcu_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw, u32 key) {
+    const u64 per = 256ull * U, npieces = (n + per - 1) / per, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u64 i = piece * per + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
+}
+
 // mode 83: as 80, plus K2's lookups between the loads and the stores: a scalar load of a
 // per-piece word from the table b, then 16 lanes load a 16-B entry it points at (entries
 // spread over 16 MB like K2's items), consumed before the stores
@@ -610,6 +627,19 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
                                0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
+    }
+    if (mode >= 880 && mode < 900) {  // 88U: U chunks per lane (1, 2, 4, 6, 8); `blocks` = unused LDS bytes per block
+        const int U = mode - 880;
+        const u32 W = 2u;
+        const u64 per = 256ull * (U > 0 ? U : 4), np = (n + per - 1) / per, ppw = (np + W - 1) / W;
+        const u32 dyn = blocks > 0 && blocks <= 65536 ? (u32)blocks : 0u;
+        if (U == 1) hipLaunchKernelGGL(ws_calib_wcu_kernel<1>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        else if (U == 2) hipLaunchKernelGGL(ws_calib_wcu_kernel<2>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        else if (U == 8) hipLaunchKernelGGL(ws_calib_wcu_kernel<8>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        else if (U == 6) hipLaunchKernelGGL(ws_calib_wcu_kernel<6>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL(ws_calib_wcu_kernel<4>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_wcu_kernel launch", e);
     }
     if (mode == 83) {  // `blocks` = number of windows; d_b: >= 18 MB (a zeroed table + items)
         const u32 W = blocks > 0 ? (u32)blocks : 2u;

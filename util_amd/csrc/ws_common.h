@@ -15,6 +15,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // Global-address-space views: hot loops must emit global_load/store, not flat_*
 // (flat ops complete out of order, so hipcc drains vmcnt+lgkmcnt before each one
 // and every load becomes its own round trip).
+// the unmask kernel's unit (ws_piece.hip K2, also behind the raw-stream path): one-shot
+// 256-thread blocks over WS_PIECE_U KiB per wave, 2^WS_PIECE_SHIFT bytes per block
+#define WS_PIECE_U 4
+#define WS_PIECE_SHIFT 14                   // 16 KiB = 256 threads * WS_PIECE_U * 16 B
 #define WS_GLOBAL __attribute__((address_space(1)))
 typedef WS_GLOBAL u32x4 gu32x4;
 typedef WS_GLOBAL u32 gu32;

@@ -29,8 +29,9 @@
 #include "ws_walk.h"
 
 #define PIECE_T 256
-#define PIECE_U 4
-#define PIECE_SHIFT 14                      // 16 KiB = PIECE_T * PIECE_U * 16 B
+#define PIECE_U WS_PIECE_U
+#define PIECE_SHIFT WS_PIECE_SHIFT
+static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's chunks");
 #define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
 #define PWALK_T 256
 

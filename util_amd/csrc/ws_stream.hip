@@ -23,7 +23,7 @@
 #include "ws_common.h"
 
 #define SPASS_T 256
-#define PIECE_SHIFT_S 14
+#define PIECE_SHIFT_S WS_PIECE_SHIFT
 
 // outcome bits packed with the candidate index: k << 36 | code << 34 | stf << 32 | (u32)ret
 //   code 1: consumed, length != g   2: consumed, walk ends (ret <= 0)   3: not consumed
