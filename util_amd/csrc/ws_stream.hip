@@ -472,22 +472,36 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
     const uintptr_t a = ((origin + cs0) & ~(uintptr_t)15) + (t % per) * RW_TPOS;
     u64 cands = 0;
     if (a < origin + len) {
+        // the thread's 64 positions and the 3 bytes after them: chunks 0..4 (chunk m only where
+        // the scalar version read it, a + 16 m < origin + len + 16; else chunk 0, masked below)
+        u32 w[4 * (RW_TPOS / 16) + 4];
 #pragma unroll
-        for (u32 j = 0; j < RW_TPOS / 16; ++j) {
-            if (a + 16 * j >= origin + len) break;                           // reads stay within len + pad
-            const u32x4 x0 = reinterpret_cast<const gu32x4*>(a)[j], x1 = reinterpret_cast<const gu32x4*>(a)[j + 1];
-            const u32 w[5] = {x0.x, x0.y, x0.z, x0.w, x1.x};
-#pragma unroll
-            for (u32 k = 0; k < 16; ++k) {
-                const u32 b0 = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                const u32 b1 = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
-                const u32 b2 = (w[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xFFu;
-                const u32 b3 = (w[(k + 3) >> 2] >> (8 * ((k + 3) & 3))) & 0xFFu;
-                const u64 pos = a + 16 * j + k - origin;
-                const bool ok = pos >= cs0 && pos < len && rw_plausible(b0, b1, b2 | b3, need_mask);
-                cands |= (u64)(ok ? 1u : 0u) << (16 * j + k);
-            }
+        for (u32 m = 0; m <= RW_TPOS / 16; ++m) {
+            const u32x4 x = reinterpret_cast<const gu32x4*>(a)[a + 16 * m < origin + len + 16 ? m : 0];
+            w[4 * m] = x.x; w[4 * m + 1] = x.y; w[4 * m + 2] = x.z; w[4 * m + 3] = x.w;
         }
+        // rw_plausible for 4 positions at once (SWAR: byte lane i = position 4q + i); the
+        // per-byte tests leave their verdict in bit 7 of each byte
+        const u32 H7 = 0x80808080u;
+        auto zb = [](u32 x) -> u32 { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };  // byte == 0
+#pragma unroll
+        for (u32 q = 0; q < RW_TPOS / 4; ++q) {
+            const u32 B0 = w[q], B1 = __builtin_amdgcn_alignbyte(w[q + 1], w[q], 1);
+            const u32 B2 = __builtin_amdgcn_alignbyte(w[q + 1], w[q], 2), B3 = __builtin_amdgcn_alignbyte(w[q + 1], w[q], 3);
+            const u32 rsv = zb(B0 & 0x70707070u);                                      // RSV bits clear
+            const u32 opc = ~(((B0 & 0x07070707u) + 0x05050505u) << 4) & H7;        // opcode & 7 <= 2
+            const u32 msk = need_mask ? (B1 & H7) : H7;                              // MASK when client
+            const u32 l64 = ~zb((B1 & 0x7F7F7F7Fu) ^ 0x7F7F7F7Fu) | zb(B2 | B3);     // len 127: top bytes 0
+            const u32 ok = rsv & opc & msk & l64 & H7;
+            const u32 bits = (((ok >> 7) * 0x00204081u) >> 21) & 15u;               // bit 8i+7 -> bit i
+            cands |= (u64)bits << (4 * q);
+        }
+        // positions inside [cs0, len) only
+        const u64 p0 = a - origin;
+        const u64 lo = cs0 > p0 ? cs0 - p0 : 0, hi = len - p0;                     // p0 < len
+        u64 rm = hi >= 64 ? ~0ull : (1ull << hi) - 1;
+        rm &= lo >= 64 ? 0ull : ~0ull << lo;
+        cands &= rm;
     }
     const u32 n = (u32)__builtin_popcountll(cands);
     u32 incl = n;                                                            // wavefront inclusive scan
