@@ -207,10 +207,12 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
  * configuration; none changes results): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse),
  * "piece_scan" (walk lanes per segment: 0 one, 1/2/3/4 64/32/16/8), "piece_whole",
- * "piece_occ", "piece_win" (log2 of the windows the unmask kernel streams side by side,
+ * "piece_occ", "piece_lds" (unused dynamic LDS per unmask block: caps its blocks per CU,
+ * default 30000 B = 5), "piece_win" (log2 of the windows the unmask kernel streams side by side,
  * default 1), "piece_wn" / "piece_wbit" (other window maps), "seg_win" / "scan_win" /
  * "enc_win" (two windows for the segment kernels / the walk; encode 1 two windows, 2
- * XCD-contiguous), "seg_lds" (unused LDS per segment block), "segfuse_cfg", "reasm_path"
+ * XCD-contiguous), "seg_lds" / "enc_lds" (unused LDS per segment / encode copy block),
+ * "segfuse_cfg", "reasm_path"
  * (0 auto, 1 fused, 2 three-kernel), "reasm_cfg", "reasm_merge", "enc_front" (encode:
  * 1 tile-scan front with the edge chunks before the copy, 0 hipcub scan and an edge
  * kernel after it), "encode_side", "encode_fused", "host_chunk_mb", "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw
