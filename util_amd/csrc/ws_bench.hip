@@ -337,6 +337,31 @@ __global__ __launch_bounds__(256) void ws_calib_wcu_kernel(gu32x4* __restrict__ 
         if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
 }
 
+// mode 89x: blocks of T threads, U chunks per lane, wave-contiguous, two windows, and
+// (SYNC) a block-level hand-off between the loads and the stores — wave 0 writes 64 words
+// to LDS, barrier, every lane reads one before storing (a block that shares one lookup of
+// its piece's frame records through LDS). `dyn` bytes of unused LDS cap blocks per CU.
+template <int T, int U, bool SYNC>
+__global__ __launch_bounds__(T) void ws_calib_blk_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw, u32 key) {
+    __shared__ u32 sh[64];
+    const u64 per = (u64)T * U, npieces = (n + per - 1) / per, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u64 i = piece * per + (threadIdx.x >> 6) * (64 * U) + (threadIdx.x & 63);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+    u32 k = key;
+    if (SYNC) {
+        if (threadIdx.x < 64) sh[threadIdx.x] = (u32)piece + threadIdx.x;
+        __syncthreads();
+        k ^= sh[(threadIdx.x * 7) & 63] & 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (i + 64u * u < n) st16<1>(v[u] ^ k, a + i + 64u * u);
+}
+
 // mode 83: as 80, plus K2's lookups between the loads and the stores: a scalar load of a
 // per-piece word from the table b, then 16 lanes load a 16-B entry it points at (entries
 // spread over 16 MB like K2's items), consumed before the stores
@@ -627,6 +652,22 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
                                0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
+    }
+    if (mode >= 890 && mode <= 895) {  // 890/891: 512 x 2 (no sync / sync); 892/893: 256 x 4; 894/895: 1024 x 1
+        const u32 W = 2u;
+        const int T = mode < 892 ? 512 : (mode < 894 ? 256 : 1024), U = 16384 / (T * 16);
+        const bool sy = mode & 1;
+        const u64 per = (u64)T * U, np = (n + per - 1) / per, ppw = (np + W - 1) / W;
+        const u32 dyn = blocks > 0 && blocks <= 65536 ? (u32)blocks : 0u;
+        const dim3 g((u32)(ppw * W));
+        if (T == 512) { if (sy) hipLaunchKernelGGL((ws_calib_blk_kernel<512, 2, true>), g, dim3(512), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+                        else hipLaunchKernelGGL((ws_calib_blk_kernel<512, 2, false>), g, dim3(512), dyn, st, a, n, W, ppw, 0x5A5A5A5Au); }
+        else if (T == 256) { if (sy) hipLaunchKernelGGL((ws_calib_blk_kernel<256, 4, true>), g, dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+                             else hipLaunchKernelGGL((ws_calib_blk_kernel<256, 4, false>), g, dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au); }
+        else { if (sy) hipLaunchKernelGGL((ws_calib_blk_kernel<1024, 1, true>), g, dim3(1024), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+               else hipLaunchKernelGGL((ws_calib_blk_kernel<1024, 1, false>), g, dim3(1024), dyn, st, a, n, W, ppw, 0x5A5A5A5Au); }
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_blk_kernel launch", e);
     }
     if (mode >= 880 && mode < 900) {  // 88U: U chunks per lane (1, 2, 4, 6, 8); `blocks` = unused LDS bytes per block
         const int U = mode - 880;
