@@ -325,11 +325,13 @@ def test_int_truncation_real_size(dev, decode_path, total):
     del gb, ob, host
 
 
-@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0)])
+@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0),
+                                     ("piece_lds", 0), ("piece_lds", 56000)])
 def test_window_mappings(dev, decode_path, opt, val):
     """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
-    blocks store nothing) and the segment kernels' two-window order (seg_win) at every
-    setting, on a batch large enough for every window to be used: bit-exact vs the oracle"""
+    blocks store nothing), the segment kernels' two-window order (seg_win) and K2's
+    blocks-per-CU cap (piece_lds: 8 and 2 blocks instead of the default 5) at every setting,
+    on a batch large enough for every window to be used: bit-exact vs the oracle"""
     W.set_option(opt, val)
     try:
         wire, off, pl, plain = wsynth.make_batch(2100, wsynth.PLEN_MIX3, 0, wsynth.B0_BINARY, 77)
@@ -344,6 +346,7 @@ def test_window_mappings(dev, decode_path, opt, val):
     finally:
         W.set_option("piece_win", 1)
         W.set_option("seg_win", 1)
+        W.set_option("piece_lds", 30000)
 
 
 def test_cfg4_shape_vs_oracle(dev, decode_path):

@@ -92,6 +92,22 @@ def test_reassemble_random_vs_oracle(dev, seed, mf):
     assert (out[~covered] == 0xEE).all()
 
 
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_reassemble_fused_geometries(dev, reasm_path, cfg):
+    """the fused kernel's other geometries (reasm_cfg 1: the compiler's occupancy, 2: 19 KiB
+    windows; default 0 = 8 waves/SIMD) give the same results, cache limit included"""
+    if reasm_path != 1:
+        pytest.skip("fused kernel option")
+    W.set_option("reasm_cfg", cfg)
+    try:
+        rng = np.random.default_rng(40 + cfg)
+        wire, so, sl = random_stream(rng, 1200)
+        check(dev, wire, so, sl, 16, tag="reasm_cfg %d" % cfg)
+        check(dev, wire, so, sl, 16, tag="reasm_cfg %d limit" % cfg, readcache_max=3000)
+    finally:
+        W.set_option("reasm_cfg", 0)
+
+
 def test_reassemble_carry_open_state(dev):
     """two batches per connection: the open state out of batch 1 is the state into batch 2"""
     rng = np.random.default_rng(21)
