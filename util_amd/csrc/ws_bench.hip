@@ -362,6 +362,26 @@ __global__ __launch_bounds__(T) void ws_calib_blk_kernel(gu32x4* __restrict__ a,
         if (i + 64u * u < n) st16<1>(v[u] ^ k, a + i + 64u * u);
 }
 
+// mode 96/97/98: out-of-place copy a -> b in E3's shape (one-shot 256 x 4 blocks over 16 KiB
+// output pieces, wave-contiguous), the source offset by 0 / 4 / 8 bytes (unaligned 16-B
+// loads, as E3's payload loads behind a header of any length)
+typedef u32x4 __attribute__((aligned(1))) cal_u32x4u;
+template <int OFF>
+__global__ __launch_bounds__(256) void ws_calib_copyoff_kernel(const unsigned char* __restrict__ a,
+                                                               gu32x4* __restrict__ b, u64 n, u32 key) {
+    const u64 npieces = (n + 1023) / 1024, last = n - 2;
+    const u64 piece = blockIdx.x;
+    if (piece >= npieces) return;
+    const u64 i = piece * 1024 + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        v[u] = *reinterpret_cast<const WS_GLOBAL cal_u32x4u*>(reinterpret_cast<uintptr_t>(a + 16 * min(i + 64u * u, last) + OFF));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (i + 64u * u < n - 1) st16<1>(v[u] ^ key, b + i + 64u * u);
+}
+
 // mode 83: as 80, plus K2's lookups between the loads and the stores: a scalar load of a
 // per-piece word from the table b, then 16 lanes load a 16-B entry it points at (entries
 // spread over 16 MB like K2's items), consumed before the stores
@@ -652,6 +672,15 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
                                0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_windows_wc_kernel launch", e);
+    }
+    if (mode >= 96 && mode <= 98) {  // d_b: >= nbytes
+        const u64 np = (n + 1023) / 1024;
+        const unsigned char* a8 = reinterpret_cast<const unsigned char*>(d_a);
+        if (mode == 96) hipLaunchKernelGGL(ws_calib_copyoff_kernel<0>, dim3((u32)np), dim3(256), 0, st, a8, b, n, 0x5A5A5A5Au);
+        else if (mode == 97) hipLaunchKernelGGL(ws_calib_copyoff_kernel<4>, dim3((u32)np), dim3(256), 0, st, a8, b, n, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL(ws_calib_copyoff_kernel<8>, dim3((u32)np), dim3(256), 0, st, a8, b, n, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_copyoff_kernel launch", e);
     }
     if (mode >= 890 && mode <= 895) {  // 890/891: 512 x 2 (no sync / sync); 892/893: 256 x 4; 894/895: 1024 x 1
         const u32 W = 2u;
