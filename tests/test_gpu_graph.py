@@ -119,12 +119,21 @@ def _streams():
     yield "random", wire, 4096                                # lengths change every frame: the walk
     w, *_ = wsynth.make_batch(5000, 0, 1000, 0, 4)
     yield "max_frames", w, 1234
+    # long streams whose lengths keep changing: the chunk-parallel walk on the device
+    w, *_ = wsynth.make_batch(3000, wsynth.PLEN_MIX3, 0, 0, 44)
+    yield "mixed_long", w, 1 << 12                           # cfg3's mix, 3000 frames (~67 MB)
+    yield "mixed_long_max_frames", w, 1777                   # ... stopped by max_frames mid-stream
+    wire, so, sl = random_stream(np.random.default_rng(45), 4000)
+    yield "random_long", wire, 1 << 15                        # quirks, unmasked frames, zero gaps
 
 
-@pytest.mark.parametrize("case", ["uniform", "runs", "random", "max_frames"])
+@pytest.mark.parametrize("case", ["uniform", "runs", "random", "max_frames", "mixed_long", "mixed_long_max_frames",
+                                  "random_long"])
 def test_stream_decode_graph_replay(dev, case):
     """websocketframeStreamDecodeDevice captured in a graph: the pass loop's state lives on
-    the device (no host reads), so the captured decode replays bit-exact"""
+    the device (no host reads), and on a long stream whose lengths keep changing the
+    chunk-parallel walk runs on the device too (plan, candidate walks, linker), so the
+    captured decode replays bit-exact"""
     name, wire, mf = next(s for s in _streams() if s[0] == case)
     n = len(wire)
     d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)

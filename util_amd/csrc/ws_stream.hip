@@ -150,7 +150,11 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned 
 // `last`: the walk runs to the stream's end (end == len) and then writes the tail
 // pointers, the item count and the segment result; otherwise it stops before the first
 // frame starting at or after `end` (another wavefront owns it).
-__device__ __forceinline__ void stream_walk(const unsigned char* __restrict__ buf, u64 len, u64 P0, u64 g0, u32 nf0,
+struct SwOut {            // where a stream_walk stopped: the next frame, its index, 1 if the walk ended
+    u64 next;
+    u32 nf, ended;
+};
+__device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ buf, u64 len, u64 P0, u64 g0, u32 nf0,
                                             u64 end, bool last, u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
                                             u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                             u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
@@ -219,7 +223,11 @@ __device__ __forceinline__ void stream_walk(const unsigned char* __restrict__ bu
         out[1] = nf;
         out[2] = at_bnd ? 0 : 1;
     }
-    if (!last && (at_bnd || !out)) return;
+    SwOut r;
+    r.next = off;
+    r.nf = nf;
+    r.ended = at_bnd ? 0u : 1u;
+    if (!last && (at_bnd || !out)) return r;
     const u32 cnt = nf + extra;
     for (u64 p = ((walked_end + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + lane;
          (p << PIECE_SHIFT_S) < lead0 + len && p < pend; p += 64)
@@ -228,6 +236,7 @@ __device__ __forceinline__ void stream_walk(const unsigned char* __restrict__ bu
         nwork[0] = cnt;
         ws_store_res(res, off, nf, status);
     }
+    return r;
 }
 
 // The rest of the stream from (P0, nf0, g0) by one wavefront (lengths that keep changing)
@@ -417,6 +426,14 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_TPOS 64        // window positions per thread
 #define RW_D 4            // distinct window exits per chunk walked on (phase B owners)
 #define RW_STG 4096       // largest staging list per owner (frame offsets); the call's is stgn
+#define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
+#define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
+
+__host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
+    u64 v = lo;
+    while (v < x && v < hi) v <<= 1;
+    return v;
+}
 
 struct RwRec {            // phase A: one surviving walk from chunk start + start
     u32 start;
@@ -430,6 +447,16 @@ struct RwOwn {            // phase B: the walk from a window exit to the chunk's
     u32 dead;             // 1: an implausible header (not the chain)
     u64 over;             // the (stgn+1)-th frame's start when more than stgn frames
     u64 pad;
+};
+
+// The walk's geometry chosen on the device (captured calls: the host cannot read the sample):
+// R1-R3, the linker and the emit take it from here; scratch is sized for the caps at capture
+struct RwPlan {
+    u64 P;                // the chunk grid's origin (the entry after the sample)
+    u64 C;                // chunk bytes
+    u32 H, nchunks, capc, stgn;
+    u32 need_mask, active, nf, nrows;
+    u64 sample_out[4];    // stream_walk's report of the sample / of a linked chunk walk
 };
 
 // b23: header bytes 2 and 3 (the top of a 64-bit length, which a real frame leaves zero:
@@ -461,10 +488,18 @@ __device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool
 // (lanes are dense in R2: a wrong start costs one lane-slot, not a wavefront-slot)
 __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
-                                                         u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc) {
-    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+                                                         u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc,
+                                                         const RwPlan* __restrict__ plan) {
+    if (plan) {                                                              // geometry from the device
+        if (!plan->active) return;
+        P = plan->P; C = plan->C; H = plan->H; nchunks = plan->nchunks; need_mask = plan->need_mask;
+        capc = plan->capc;
+    }
     const u32 lane = threadIdx.x & 63;
     const u32 per = H / RW_TPOS;                                             // a multiple of 64: one
+    // grid-stride (a captured call's grid is sized for the largest geometry); a whole
+    // wavefront takes the same iterations
+    for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x;; t += (u64)gridDim.x * 256) {
     const u64 c = t / per;                                                   // chunk per wavefront
     if (c >= nchunks) return;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
@@ -522,6 +557,7 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         if (o < capc) cl[o] = a + k - origin;
         ++o;
     }
+    }
 }
 
 // R2 (window walks): one lane per candidate (grid-stride), the walk to the window's end
@@ -531,7 +567,13 @@ __global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
                                                          const u64* __restrict__ cand, u32 capc,
                                                          RwRec* __restrict__ recs, u32* __restrict__ nrec,
-                                                         unsigned long long* __restrict__ dx) {
+                                                         unsigned long long* __restrict__ dx,
+                                                         const RwPlan* __restrict__ plan) {
+    if (plan) {
+        if (!plan->active) return;
+        P = plan->P; C = plan->C; H = plan->H; nchunks = plan->nchunks; need_mask = plan->need_mask;
+        capc = plan->capc;
+    }
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
     const u64 n = (u64)nchunks * capc;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
@@ -577,7 +619,12 @@ __global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __
 __global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
                                                         u32 nchunks, u32 need_mask,
                                                         const unsigned long long* __restrict__ dx,
-                                                        RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn) {
+                                                        RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn,
+                                                        const RwPlan* __restrict__ plan) {
+    if (plan) {
+        if (!plan->active) return;
+        P = plan->P; C = plan->C; nchunks = plan->nchunks; need_mask = plan->need_mask; stgn = plan->stgn;
+    }
     const u64 oi = (u64)blockIdx.x * 256 + threadIdx.x;
     if (oi >= (u64)nchunks * RW_D) return;
     u64 pos = dx[oi];
@@ -613,7 +660,12 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
                                                         const u32* __restrict__ stg, u32 stgn,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
-                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
+                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
+                                                        const RwPlan* __restrict__ plan) {
+    if (plan) {                                                              // rows written by the linker
+        if (!plan->active || blockIdx.x >= plan->nrows) return;
+        stgn = plan->stgn;
+    }
     const u64* t = tab + 8 * blockIdx.x;
     const u64 ent = t[0], exit_w = t[1], nf0 = t[2], cnt_w = t[3], oi = t[4], n_par = t[5], cs0 = t[7];
     const bool last = t[6] != 0;
@@ -652,10 +704,175 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
                 ptr, pend, nwork, res, lane);
 }
 
+// ---- the chunk-parallel walk inside a captured call (no host reads): the plan kernel
+// walks the sample and picks the geometry, R1-R3 read it, the linker follows the records
+// on the device (the host loop of rw_walk, one wavefront), the emit writes the chain.
+#define RW_CAP_CHUNKS 32768u   // a captured call's chunk-count cap (the smallest chunk follows)
+#define RW_CAP_STGN 1024u      // ... and staging per owner
+
+__global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __restrict__ buf, u64 len, u32 max_frames,
+                                                        const SdState* __restrict__ sd, RwPlan* __restrict__ plan,
+                                                        u64 cmin, u64 cmax, u32 nchunks_cap, u64 cand_cap, u64 stg_cap,
+                                                        WebsocketFrameDesc_t* __restrict__ desc,
+                                                        u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
+                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
+    const u32 lane = threadIdx.x;
+    if (sd->phase == SD_DONE) {                                              // the passes finished it
+        if (lane == 0) plan->active = 0;
+        return;
+    }
+    const u64 P = sd->P;
+    const u32 nf = sd->nf;
+    // the sample (a walk that ends in it finishes the stream: `out` given)
+    const u64 send = len - P > RW_SAMPLE ? P + RW_SAMPLE : len;
+    const SwOut o = stream_walk(buf, len, P, sd->g, nf, send, false, max_frames, desc, items, ptr, pend, nwork, res,
+                                lane, plan->sample_out);
+    if (o.ended) {
+        if (lane == 0) plan->active = 0;
+        return;
+    }
+    const u64 P1 = o.next;
+    const u64 mean = o.nf > nf ? (P1 - P) / (o.nf - nf) : (P1 - P);
+    if ((len - P1) / (mean ? mean : 1) < RW_MIN_FRAMES) {                   // a short rest: this wavefront
+        stream_walk(buf, len, P1, 0, o.nf, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
+        if (lane == 0) plan->active = 0;
+        return;
+    }
+    u64 C = rw_pow2_clamp(mean * 1024, cmin > RW_CMIN ? cmin : RW_CMIN, cmin > cmax ? cmin : cmax);
+    u64 nch = (len - P1 + C - 1) / C;
+    // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
+    while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
+    const u32 H = (u32)rw_pow2_clamp(mean * 8, RW_HMIN, C / 2 < RW_HMAX ? C / 2 : RW_HMAX);
+    u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
+    while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
+    u64 capc = H / 32;
+    while (capc > 64 && nch * capc > cand_cap) capc >>= 1;
+    if (lane == 0) {
+        plan->P = P1;
+        plan->C = C;
+        plan->H = H;
+        plan->nchunks = (u32)nch;
+        plan->capc = (u32)capc;
+        plan->stgn = (u32)stgn;
+        plan->need_mask = (buf[P1 + 1] & 0x80u) ? 1u : 0u;                   // client frames: masked
+        plan->nf = o.nf;
+        plan->nrows = 0;
+        plan->active = 1;
+    }
+}
+
+// The linker: from the plan's entry, chunk by chunk, the record whose start is the entry
+// (A records, then the walks that end the stream), its window exit's owner walk, one
+// emit row per chunk; a chunk without a usable record is walked here by this wavefront
+// (stream_walk writes its frames; a walk that ends the stream finishes it). Bounded by
+// the chunk count (every step moves the entry forward).
+__global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __restrict__ buf, u64 len, u32 max_frames,
+                                                        RwPlan* __restrict__ plan, const RwRec* __restrict__ recs,
+                                                        const u32* __restrict__ nrec,
+                                                        const unsigned long long* __restrict__ dx,
+                                                        const RwOwn* __restrict__ own, u64* __restrict__ tab,
+                                                        WebsocketFrameDesc_t* __restrict__ desc,
+                                                        u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
+                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
+    const u32 lane = threadIdx.x;
+    if (!plan->active) return;
+    const u64 P = plan->P, C = plan->C;
+    const u32 H = plan->H, nchunks = plan->nchunks, stgn = plan->stgn;
+    u64 ent = P;
+    u32 nfc = plan->nf, rows = 0;
+    bool last = false;
+    auto row = [&](u64 a0, u64 a1, u64 a2, u64 a3, u64 a4, u64 a5, u64 a6, u64 a7) {
+        if (lane == 0) {
+            u64* t = tab + 8 * (u64)rows;
+            t[0] = a0; t[1] = a1; t[2] = a2; t[3] = a3; t[4] = a4; t[5] = a5; t[6] = a6; t[7] = a7;
+        }
+        ++rows;
+    };
+    for (u32 it = 0; it <= nchunks + 1 && !last && ent < len; ++it) {
+        const u64 c = (ent - P) / C, cs0 = P + c * C;
+        bool found = false;
+        RwRec r = {};
+        if (c < nchunks && ent - cs0 < H) {
+            const u32 so = (u32)(ent - cs0);
+            const bool lastc = c + 1 == nchunks;
+            const u32 n0 = nrec[4 * c], n1 = nrec[4 * c + 1];
+            const u32 na = n0 < RW_S0 ? n0 : RW_S0;
+            RwRec q = {};
+            if (lane < na) q = recs[c * RW_SLOTS + lane];
+            u64 m = __ballot(lane < na && q.start == so);
+            if (m) {
+                const int i = __builtin_ctzll(m);
+                r.start = so;
+                r.cs = (u32)__builtin_amdgcn_readlane((int)q.cs, i);
+                r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q.exit, i)) |
+                         ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q.exit >> 32), i) << 32);
+                found = true;
+            } else {                                                         // walks that end the stream
+                const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
+                const u32 nb1 = lastc ? (n1 < RW_SLAST ? n1 : RW_SLAST) : (n1 < RW_S1 ? n1 : RW_S1);
+                for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
+                    RwRec q1 = {};
+                    if (k0 + lane < nb1) q1 = r1[k0 + lane];
+                    const u64 m1 = __ballot(k0 + lane < nb1 && q1.start == so);
+                    if (m1) {
+                        const int i = __builtin_ctzll(m1);
+                        r.start = so;
+                        r.cs = (u32)__builtin_amdgcn_readlane((int)q1.cs, i);
+                        r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q1.exit, i)) |
+                                 ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q1.exit >> 32), i) << 32);
+                        found = true;
+                    }
+                }
+            }
+        }
+        const u32 cnt_w = found ? (r.cs & 0x7FFFFFFFu) : 0u;
+        if (found && ((r.cs >> 31) || (u64)nfc + cnt_w >= max_frames)) {   // ends in the window: group walk
+            row(ent, 0, nfc, 0, ~0ull, 0, 1, cs0);
+            last = true;
+            break;
+        }
+        if (found) {
+            // the owner walk of this exit (at most RW_D distinct exits per chunk)
+            unsigned long long d = 0;
+            RwOwn ow = {};
+            if (lane < RW_D) {
+                d = dx[c * RW_D + lane];
+                ow = own[c * RW_D + lane];
+            }
+            const u64 mo = __ballot(lane < RW_D && d == r.exit);
+            if (mo) {
+                const int i = __builtin_ctzll(mo);
+                const u32 dead = (u32)__builtin_amdgcn_readlane((int)ow.dead, i);
+                if (!dead) {
+                    const u32 ocs = (u32)__builtin_amdgcn_readlane((int)ow.cs, i);
+                    const u64 oexit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)ow.exit, i)) |
+                                      ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(ow.exit >> 32), i) << 32);
+                    const u32 nb = ocs & 0x7FFFFFFFu;
+                    last = (ocs >> 31) != 0 || oexit >= len || (u64)nfc + cnt_w + nb >= max_frames;
+                    u64 n_par = nb < stgn ? nb : stgn;
+                    if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
+                    row(ent, r.exit, nfc, cnt_w, c * RW_D + (u64)i, n_par, last ? 1ull : 0ull, cs0);
+                    nfc += cnt_w + nb;
+                    ent = oexit;
+                    continue;
+                }
+            }
+        }
+        // no usable record: this wavefront walks the chunk (writing its frames)
+        const SwOut o = stream_walk(buf, len, ent, 0, nfc, cs0 + C < len ? cs0 + C : len, false, max_frames, desc,
+                                    items, ptr, pend, nwork, res, lane, plan->sample_out);
+        if (o.ended) { last = true; break; }                                // (the walk finished the stream)
+        if (o.next <= ent) break;                                            // (cannot happen: no progress)
+        ent = o.next;
+        nfc = o.nf;
+    }
+    if (!last)                                                               // safety: walk whatever is left
+        stream_walk(buf, len, ent, 0, nfc, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
+    if (lane == 0) plan->nrows = rows;
+}
+
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
 
-#define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
-#define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
 WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
@@ -680,11 +897,6 @@ static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch* o
     return 0;
 }
 
-static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
-    u64 v = lo;
-    while (v < x && v < hi) v <<= 1;
-    return v;
-}
 
 // The chunk-parallel walk of [P, len) with nf frames before P (see above). Launches the
 // emit kernels and, for chunks without a link, one-wavefront chunk walks; the last of
@@ -770,14 +982,14 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const u32 need_mask = (hb[1] & 0x80u) ? 1u : 0u;
     const u64 threads = nchunks * (H / RW_TPOS);
     hipLaunchKernelGGL(ws_rw_cand_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
-                       (u32)nchunks, need_mask, cand, nrec, capc);
+                       (u32)nchunks, need_mask, cand, nrec, capc, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_cand_kernel launch", e);
     const u32 r2_blocks = (u32)std::min<u64>((nchunks * capc + 255) / 256, 4096);  // grid-stride
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
-                       need_mask, cand, capc, recs, nrec, dx);
+                       need_mask, cand, capc, recs, nrec, dx, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
     hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len, P,
-                       C, (u32)nchunks, need_mask, dx, own, stg, stgn);
+                       C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
@@ -846,11 +1058,72 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         if ((e = hipMemcpyAsync(tab, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stream chain)", e);
         hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nblk), dim3(64), 0, st, d_buf, len, max_frames, tab, own, stg, stgn,
-                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, (const RwPlan*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_emit_kernel launch", e);
     }
     // `ht` is pageable host memory read by the copy above: complete it before returning
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+    return 0;
+}
+
+// A captured call's chunk-parallel walk: scratch sized from the stream length (caps), the
+// geometry chosen on the device (ws_rw_plan_kernel). Layout after the aux head.
+struct RwDevLayout {
+    u64 cmin, nch_cap, cand_cap, stg_cap;
+    size_t o_plan, o_recs, o_nrec, o_dx, o_own, o_tab, o_stg, o_cand, bytes, zero_bytes;
+};
+static RwDevLayout rw_dev_layout(u64 len) {
+    RwDevLayout L;
+    L.cmin = RW_CMIN;
+    while ((len + L.cmin - 1) / L.cmin + 2 > RW_CAP_CHUNKS) L.cmin <<= 1;
+    L.nch_cap = (len + L.cmin - 1) / L.cmin + 2;
+    L.cand_cap = std::min<u64>(L.nch_cap * (RW_HMAX / 32), len / 1024 + 65536);
+    L.stg_cap = std::min<u64>(L.nch_cap * RW_D * RW_CAP_STGN, len / 256 + 65536);
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t o = 0;
+    L.o_plan = o; o += up(sizeof(RwPlan));
+    L.o_nrec = o; o += up(L.nch_cap * 16);                                   // zeroed: counters,
+    L.o_dx = o; o += up(L.nch_cap * RW_D * 8);                               // claimed exits
+    L.zero_bytes = o - L.o_nrec;
+    L.o_recs = o; o += up((L.nch_cap * RW_SLOTS + RW_SLAST) * sizeof(RwRec));
+    L.o_own = o; o += up(L.nch_cap * RW_D * sizeof(RwOwn));
+    L.o_tab = o; o += up((L.nch_cap + 2) * 64);
+    L.o_stg = o; o += up(L.stg_cap * 4);
+    L.o_cand = o; o += up(L.cand_cap * 8);
+    L.bytes = o;
+    return L;
+}
+
+static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, WebsocketFrameDesc_t* d_desc,
+                          const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st, const SdState* sd,
+                          unsigned char* w, const RwDevLayout& L) {
+    RwPlan* plan = reinterpret_cast<RwPlan*>(w + L.o_plan);
+    u32* nrec = reinterpret_cast<u32*>(w + L.o_nrec);
+    unsigned long long* dx = reinterpret_cast<unsigned long long*>(w + L.o_dx);
+    RwRec* recs = reinterpret_cast<RwRec*>(w + L.o_recs);
+    RwOwn* own = reinterpret_cast<RwOwn*>(w + L.o_own);
+    u64* tab = reinterpret_cast<u64*>(w + L.o_tab);
+    u32* stg = reinterpret_cast<u32*>(w + L.o_stg);
+    u64* cand = reinterpret_cast<u64*>(w + L.o_cand);
+    const u64 cmax = ws_stream_rw_cmax >= 16 && ws_stream_rw_cmax <= 26 ? 1ull << ws_stream_rw_cmax : RW_CMAX;
+    hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
+    if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
+    hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
+                       (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+    // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
+    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+                       cand, nrec, 0u, (const RwPlan*)plan);
+    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+                       (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
+                       (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
+    hipLaunchKernelGGL(ws_rw_link_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, plan, (const RwRec*)recs,
+                       (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, tab, d_desc, Pw.items,
+                       Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+    hipLaunchKernelGGL(ws_rw_emit_kernel, dim3((u32)(L.nch_cap + 2)), dim3(64), 0, st, d_buf, len, max_frames,
+                       (const u64*)tab, (const RwOwn*)own, (const u32*)stg, 0u, d_desc, Pw.items, Pw.ptr, Pw.npieces,
+                       Pw.nwork, d_res, (const RwPlan*)plan);
+    if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("stream walk (device) launch", e);
     return 0;
 }
 
@@ -879,8 +1152,12 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     // call (and any shorter stream) never reads it: `nr` rounds, the last one's resolve also
     // walks whatever is left with one wavefront.
     const bool host_rw = ws_stream_rw && len >= RW_MIN && !capture;
+    // a captured call on a long stream runs the chunk-parallel walk on the device (its
+    // scratch, sized from the length, follows the state in the aux workspace)
+    const bool dev_rw = ws_stream_rw && len >= RW_MIN && capture;
+    const RwDevLayout RL = dev_rw ? rw_dev_layout(len) : RwDevLayout{};
     WsAux A;
-    if ((rc = ws_aux_workspace(WS_AUX_HEAD, host_rw ? WS_AUX_HEAD : 0, st, &A))) return rc;
+    if ((rc = ws_aux_workspace(WS_AUX_HEAD + (dev_rw ? RL.bytes : 0), host_rw ? WS_AUX_HEAD : 0, st, &A))) return rc;
     SdState* sd = reinterpret_cast<SdState*>(A.d);
     SdMirror* hm = host_rw ? reinterpret_cast<SdMirror*>(A.h) : nullptr;
     SdMirror* dm = host_rw ? reinterpret_cast<SdMirror*>(A.h_dev) : nullptr;
@@ -926,6 +1203,14 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
     const int nr = ws_stream_rounds >= 1 && ws_stream_rounds <= 64 ? (int)ws_stream_rounds : 4;
+    if (dev_rw) {
+        if ((rc = rounds(nr, false, 0))) return rc;
+        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
+                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL)))
+            return rc;
+        *A.state_ok = true;
+        return ws_launch_piece_unmask(L, Pw, 1, gen);
+    }
     if (!host_rw) {
         if ((rc = rounds(nr, true, 0))) return rc;
         *A.state_ok = true;
