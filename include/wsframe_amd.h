@@ -189,8 +189,10 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
  * after d_buf + len. Frame boundaries are found by grid-wide speculative passes (one
  * probe + rest pair per change of frame length); the loop's state stays on the device (the
  * last block of each pass applies its stop), so the call is asynchronous and may be
- * captured in a HIP graph: "stream_rounds" pass pairs (default 4), then one wavefront
- * walks whatever is left. An eager call on a stream of >= 512 KiB reads the state back
+ * captured in a HIP graph: "stream_rounds" pass pairs (default 4), then, on a stream of
+ * >= 512 KiB, the chunk-parallel walk below with its geometry chosen and its chunk records
+ * linked on the device (scratch sized from len when captured: about 2-5 % of len), on a
+ * shorter one a single wavefront. An eager call on a stream of >= 512 KiB reads the state back
  * after every such group of rounds (one small device-to-host copy, synchronizing
  * hip_stream): more rounds while they pay, and once lengths keep changing (>= 512 KiB and
  * >= 256 frames left) a chunk-parallel walk (speculative chunk entries, chunks of ~1024
