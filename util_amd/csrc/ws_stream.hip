@@ -788,83 +788,101 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
         }
         ++rows;
     };
-    for (u32 it = 0; it <= nchunks + 1 && !last && ent < len; ++it) {
-        const u64 c = (ent - P) / C, cs0 = P + c * C;
-        bool found = false;
-        RwRec r = {};
-        if (c < nchunks && ent - cs0 < H) {
-            const u32 so = (u32)(ent - cs0);
-            const bool lastc = c + 1 == nchunks;
-            const u32 n0 = nrec[4 * c], n1 = nrec[4 * c + 1];
-            const u32 na = n0 < RW_S0 ? n0 : RW_S0;
-            RwRec q = {};
-            if (lane < na) q = recs[c * RW_SLOTS + lane];
-            u64 m = __ballot(lane < na && q.start == so);
-            if (m) {
-                const int i = __builtin_ctzll(m);
-                r.start = so;
-                r.cs = (u32)__builtin_amdgcn_readlane((int)q.cs, i);
-                r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q.exit, i)) |
-                         ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q.exit >> 32), i) << 32);
-                found = true;
-            } else {                                                         // walks that end the stream
-                const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
-                const u32 nb1 = lastc ? (n1 < RW_SLAST ? n1 : RW_SLAST) : (n1 < RW_S1 ? n1 : RW_S1);
-                for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
-                    RwRec q1 = {};
-                    if (k0 + lane < nb1) q1 = r1[k0 + lane];
-                    const u64 m1 = __ballot(k0 + lane < nb1 && q1.start == so);
-                    if (m1) {
-                        const int i = __builtin_ctzll(m1);
-                        r.start = so;
-                        r.cs = (u32)__builtin_amdgcn_readlane((int)q1.cs, i);
-                        r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q1.exit, i)) |
-                                 ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q1.exit >> 32), i) << 32);
-                        found = true;
+    // The records of RW_LK consecutive chunks are loaded in one round (the chain almost always
+    // moves to the next chunk), then taken one chunk at a time; a chain that leaves that run
+    // (a skipped chunk, a chunk walked here) reloads at its new chunk.
+    constexpr u32 RW_LK = 8;
+    u32 steps = 0;
+    while (!last && ent < len && steps <= nchunks + 1) {
+        const u64 c0 = (ent - P) / C;
+        u32 n0[RW_LK], n1[RW_LK];
+        RwRec q[RW_LK];
+        unsigned long long dd[RW_LK];
+        RwOwn oo[RW_LK];
+#pragma unroll
+        for (u32 k = 0; k < RW_LK; ++k) {                                   // clamped: in-range loads
+            const u64 cc = c0 + k < nchunks ? c0 + k : (nchunks ? nchunks - 1 : 0);
+            n0[k] = nrec[4 * cc];
+            n1[k] = nrec[4 * cc + 1];
+            q[k] = recs[cc * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
+            dd[k] = dx[cc * RW_D + (lane & (RW_D - 1))];
+            oo[k] = own[cc * RW_D + (lane & (RW_D - 1))];
+        }
+        bool reload = false;
+#pragma unroll
+        for (u32 k = 0; k < RW_LK; ++k) {
+            if (reload || last || ent >= len) break;
+            const u64 c = (ent - P) / C, cs0 = P + c * C;
+            if (c != c0 + k) break;                                          // left the run: reload
+            ++steps;
+            bool found = false;
+            RwRec r = {};
+            if (c < nchunks && ent - cs0 < H) {
+                const u32 so = (u32)(ent - cs0);
+                const bool lastc = c + 1 == nchunks;
+                const u32 na = n0[k] < RW_S0 ? n0[k] : RW_S0;
+                const u64 m = __ballot(lane < na && q[k].start == so);
+                if (m) {
+                    const int i = __builtin_ctzll(m);
+                    r.start = so;
+                    r.cs = (u32)__builtin_amdgcn_readlane((int)q[k].cs, i);
+                    r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q[k].exit, i)) |
+                             ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q[k].exit >> 32), i) << 32);
+                    found = true;
+                } else {                                                     // walks that end the stream
+                    const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
+                    const u32 nb1 = lastc ? (n1[k] < RW_SLAST ? n1[k] : RW_SLAST) : (n1[k] < RW_S1 ? n1[k] : RW_S1);
+                    for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
+                        RwRec q1 = {};
+                        if (k0 + lane < nb1) q1 = r1[k0 + lane];
+                        const u64 m1 = __ballot(k0 + lane < nb1 && q1.start == so);
+                        if (m1) {
+                            const int i = __builtin_ctzll(m1);
+                            r.start = so;
+                            r.cs = (u32)__builtin_amdgcn_readlane((int)q1.cs, i);
+                            r.exit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)q1.exit, i)) |
+                                     ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q1.exit >> 32), i) << 32);
+                            found = true;
+                        }
                     }
                 }
             }
-        }
-        const u32 cnt_w = found ? (r.cs & 0x7FFFFFFFu) : 0u;
-        if (found && ((r.cs >> 31) || (u64)nfc + cnt_w >= max_frames)) {   // ends in the window: group walk
-            row(ent, 0, nfc, 0, ~0ull, 0, 1, cs0);
-            last = true;
-            break;
-        }
-        if (found) {
-            // the owner walk of this exit (at most RW_D distinct exits per chunk)
-            unsigned long long d = 0;
-            RwOwn ow = {};
-            if (lane < RW_D) {
-                d = dx[c * RW_D + lane];
-                ow = own[c * RW_D + lane];
+            const u32 cnt_w = found ? (r.cs & 0x7FFFFFFFu) : 0u;
+            if (found && ((r.cs >> 31) || (u64)nfc + cnt_w >= max_frames)) { // ends in the window: group walk
+                row(ent, 0, nfc, 0, ~0ull, 0, 1, cs0);
+                last = true;
+                break;
             }
-            const u64 mo = __ballot(lane < RW_D && d == r.exit);
-            if (mo) {
-                const int i = __builtin_ctzll(mo);
-                const u32 dead = (u32)__builtin_amdgcn_readlane((int)ow.dead, i);
-                if (!dead) {
-                    const u32 ocs = (u32)__builtin_amdgcn_readlane((int)ow.cs, i);
-                    const u64 oexit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)ow.exit, i)) |
-                                      ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(ow.exit >> 32), i) << 32);
-                    const u32 nb = ocs & 0x7FFFFFFFu;
-                    last = (ocs >> 31) != 0 || oexit >= len || (u64)nfc + cnt_w + nb >= max_frames;
-                    u64 n_par = nb < stgn ? nb : stgn;
-                    if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
-                    row(ent, r.exit, nfc, cnt_w, c * RW_D + (u64)i, n_par, last ? 1ull : 0ull, cs0);
-                    nfc += cnt_w + nb;
-                    ent = oexit;
-                    continue;
+            if (found) {
+                // the owner walk of this exit (at most RW_D distinct exits per chunk)
+                const u64 mo = __ballot(lane < RW_D && dd[k] == r.exit);
+                if (mo) {
+                    const int i = __builtin_ctzll(mo);
+                    const u32 dead = (u32)__builtin_amdgcn_readlane((int)oo[k].dead, i);
+                    if (!dead) {
+                        const u32 ocs = (u32)__builtin_amdgcn_readlane((int)oo[k].cs, i);
+                        const u64 oexit = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)oo[k].exit, i)) |
+                                          ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(oo[k].exit >> 32), i) << 32);
+                        const u32 nb = ocs & 0x7FFFFFFFu;
+                        last = (ocs >> 31) != 0 || oexit >= len || (u64)nfc + cnt_w + nb >= max_frames;
+                        u64 n_par = nb < stgn ? nb : stgn;
+                        if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
+                        row(ent, r.exit, nfc, cnt_w, c * RW_D + (u64)i, n_par, last ? 1ull : 0ull, cs0);
+                        nfc += cnt_w + nb;
+                        ent = oexit;
+                        continue;
+                    }
                 }
             }
+            // no usable record: this wavefront walks the chunk (writing its frames)
+            const SwOut o = stream_walk(buf, len, ent, 0, nfc, cs0 + C < len ? cs0 + C : len, false, max_frames, desc,
+                                        items, ptr, pend, nwork, res, lane, plan->sample_out);
+            if (o.ended) { last = true; break; }                            // (the walk finished the stream)
+            if (o.next <= ent) { steps = nchunks + 2; break; }               // (cannot happen: no progress)
+            ent = o.next;
+            nfc = o.nf;
+            reload = true;                                                   // its frames may cross chunks
         }
-        // no usable record: this wavefront walks the chunk (writing its frames)
-        const SwOut o = stream_walk(buf, len, ent, 0, nfc, cs0 + C < len ? cs0 + C : len, false, max_frames, desc,
-                                    items, ptr, pend, nwork, res, lane, plan->sample_out);
-        if (o.ended) { last = true; break; }                                // (the walk finished the stream)
-        if (o.next <= ent) break;                                            // (cannot happen: no progress)
-        ent = o.next;
-        nfc = o.nf;
     }
     if (!last)                                                               // safety: walk whatever is left
         stream_walk(buf, len, ent, 0, nfc, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
