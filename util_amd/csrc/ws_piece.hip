@@ -323,6 +323,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                 const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
 #pragma unroll
                 for (int u = 0; u < PIECE_U; ++u) {
+                    if (b <= u * 1024 || a >= u * 1024 + 1024) continue;       // (uniform) not in row u
                     const int x = u * 1024 + xl;
                     const int lo = a > x ? a - x : 0, hi = b < x + 16 ? b - x : 16;
                     if (hi <= lo) continue;
