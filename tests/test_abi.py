@@ -235,3 +235,30 @@ def test_channel_glue_batch_replay(case):
     got, got_off = _reactor_loop(batch, lambda p, n, r: lib.websocketframeOnDecodeBatch(C.byref(cur), p, n, r))
     assert got == ref and got_off == ref_off
     assert np.array_equal(batch[:ref_off], single[:ref_off])
+
+
+OPTION_CHECK = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from util_amd import wsframe as W
+names = sys.argv[2].split(",")
+VAL = {"unroll": 4}                                         # (unroll takes 2, 4 or 8)
+bad = [n for n in names if W.load_lib().websocketframeGpuSetOption(n.encode(), VAL.get(n, 1)) != 0]
+unknown_ok = W.load_lib().websocketframeGpuSetOption(b"no_such_option", 1) == 0
+print("BAD", bad, "UNKNOWN_ACCEPTED", unknown_ok)
+sys.exit(1 if bad or unknown_ok else 0)
+"""
+
+
+def test_documented_options_are_accepted():
+    """every tuning knob the header documents for websocketframeGpuSetOption is accepted by the
+    library and an unknown name is refused (checked in a child process: setting options is
+    process-global state)"""
+    hdr = open(os.path.join(_lib.REPO, "include", "wsframe_amd.h")).read()
+    block = hdr[hdr.index("/* Launch tuning knobs"):hdr.index("WSFRAME_AMD_EXPORT int websocketframeGpuSetOption")]
+    names = sorted(set(re.findall(r'"([a-z0-9_]+)"', block)))
+    assert "piece_lds" in names and "enc_lds" in names and "reasm_cfg" in names, names
+    util_amd.load_lib()
+    r = subprocess.run([os.environ.get("PYTHON", "python3"), "-c", OPTION_CHECK, _lib.REPO, ",".join(names)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
