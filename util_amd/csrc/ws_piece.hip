@@ -262,12 +262,23 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     const u64 r0 = wc0 << 4, r1 = r0 + RW;
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
         reinterpret_cast<uintptr_t>(ptr + pidx));
+    // the next piece's first item: when it is in the same segment, the items that touch this
+    // piece are exactly [k, k_next], so the first load takes only those (long segments would
+    // otherwise load 16 per wave however few they need)
+    const u64 pn = pidx + 1 < npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+                                            reinterpret_cast<uintptr_t>(ptr + pidx + 1))
+                                      : PIECE_NONE;
     const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
     u32 cov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) cov[u] = 0;
     // no early return: an exit branch here would be hoisted above the payload loads
     u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv, step = 16;
+    bool exact = false;                                                     // the first load holds them all
+    if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
+        step = (u32)pn - k + 1;
+        exact = true;
+    }
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                     ws_xor_range(key, lo, hi, v[u], cov[u]);                    // unmask in registers
                 }
             }
-            if (nlim < step) break;                                         // reached an item past the range
+            if (nlim < step || exact) break;                                // reached an item past the range
             if (k + step < cnt) { k += step; step = 64; continue; }         // more items of this segment
         }
         // this segment has no more items: continue with the next one if it starts in range
