@@ -795,15 +795,20 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     u32 steps = 0;
     while (!last && ent < len && steps <= nchunks + 1) {
         const u64 c0 = (ent - P) / C;
-        u32 n0[RW_LK], n1[RW_LK];
+        // lane l < RW_LK: the record counts of chunk c0 + l (read back per chunk by readlane)
+        u32 n0v = 0, n1v = 0;
+        {
+            const u64 cl = c0 + (lane < RW_LK ? lane : 0);
+            const u64 cc = cl < nchunks ? cl : (nchunks ? nchunks - 1 : 0);
+            n0v = nrec[4 * cc];
+            n1v = nrec[4 * cc + 1];
+        }
         RwRec q[RW_LK];
         unsigned long long dd[RW_LK];
         RwOwn oo[RW_LK];
 #pragma unroll
         for (u32 k = 0; k < RW_LK; ++k) {                                   // clamped: in-range loads
             const u64 cc = c0 + k < nchunks ? c0 + k : (nchunks ? nchunks - 1 : 0);
-            n0[k] = nrec[4 * cc];
-            n1[k] = nrec[4 * cc + 1];
             q[k] = recs[cc * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
             dd[k] = dx[cc * RW_D + (lane & (RW_D - 1))];
             oo[k] = own[cc * RW_D + (lane & (RW_D - 1))];
@@ -820,7 +825,9 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
             if (c < nchunks && ent - cs0 < H) {
                 const u32 so = (u32)(ent - cs0);
                 const bool lastc = c + 1 == nchunks;
-                const u32 na = n0[k] < RW_S0 ? n0[k] : RW_S0;
+                const u32 n0k = (u32)__builtin_amdgcn_readlane((int)n0v, (int)k);
+                const u32 n1k = (u32)__builtin_amdgcn_readlane((int)n1v, (int)k);
+                const u32 na = n0k < RW_S0 ? n0k : RW_S0;
                 const u64 m = __ballot(lane < na && q[k].start == so);
                 if (m) {
                     const int i = __builtin_ctzll(m);
@@ -831,7 +838,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                     found = true;
                 } else {                                                     // walks that end the stream
                     const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
-                    const u32 nb1 = lastc ? (n1[k] < RW_SLAST ? n1[k] : RW_SLAST) : (n1[k] < RW_S1 ? n1[k] : RW_S1);
+                    const u32 nb1 = lastc ? (n1k < RW_SLAST ? n1k : RW_SLAST) : (n1k < RW_S1 ? n1k : RW_S1);
                     for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
                         RwRec q1 = {};
                         if (k0 + lane < nb1) q1 = r1[k0 + lane];
