@@ -257,9 +257,11 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
     u32 kind[ENC_U];                                                          // 1: inside one payload
 #pragma unroll
     for (int u = 0; u < ENC_U; ++u) { kind[u] = 0; fsrc[u] = 0; fkey[u] = 0; }
-    for (u32 k = first; k < n;) {
+    // records load `step` at a time: 16 first (a 4 KiB wave range rarely needs more), 64 after
+    // that — 64 lanes loading would fetch 2 KiB of records per wave, into every XCD's L2
+    for (u32 k = first, step = 16; k < n;) {
         const u32 j = k + lane;
-        const bool valid = j < n;
+        const bool valid = j < n && lane < step;
         EncFrame e = {};
         if (valid) e = enc_load(f, wire_off, j);
         const u64 eo = e.off + lead0, ee = eo + e.hl + e.len;                // origin-relative extent
@@ -306,12 +308,13 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
             nx.masked = __shfl_down(e.masked, 1, 64);
             const bool nxt = j + 1 < n;
             const bool mine = valid && lane < nlim && ee > r0;
-            if (mine && lane == 63 && nxt) nx = enc_load(f, wire_off, j + 1);
+            if (mine && lane == step - 1 && nxt) nx = enc_load(f, wire_off, j + 1);
             if (mine && enc_edge_eligible(e, nx, j, n, lead0, out_lo, out_hi))
                 enc_edge_store(src, base, e, nx, nxt, lead0, r0, r1);
         }
-        if (nlim < 64) break;
-        k += 64;
+        if (nlim < step) break;
+        k += step;
+        step = 64;
     }
     // payload-interior chunks: one unaligned 16-B source load each (issued together)
     u32x4 v[ENC_U];
