@@ -33,10 +33,12 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
-KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel"}
+KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel", 5: "ws_piece_spec_kernel"}
 STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel (which decodes unordered batches itself, "
                    "one wave per segment)",
-                4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)"}
+                4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)",
+                5: "ws_piece_spec_kernel (speculative frame grid, verified in the unmask) + ws_piece_spec_fix_kernel "
+                   "(repair of mispredicted segments; exits at once when there are none)"}
 DEFAULT_PATH = -1  # auto: 4 (segfuse) for >= 1024 segments of <= 17 KiB - 64 B average, max_frames <= 64; else 3
 
 
@@ -913,7 +915,9 @@ def main():
         def step():
             graph.replay()
             wl.decodes += 1
+    spec0 = wl.W.get_stat("piece_spec_calls")
     elapsed, step_ms = timed_region(step, args.steps, world)
+    spec_steps = wl.W.get_stat("piece_spec_calls") - spec0          # path 3: calls that took the speculative form
     kern_ms = np.array([step_ms])
     from util_amd import dist as D
     elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
@@ -923,8 +927,10 @@ def main():
     # k2_timing), over a second region of the same calls (events between kernels would
     # perturb the contract's region above, so it is not timed this way)
     kpath = decode_path(path, wl)
+    if kpath == 3 and spec_steps == args.steps:
+        kpath = 5                                                   # every timed call was speculative
     k2_ms = None
-    if kpath == 3 and not args.graph:
+    if kpath in (3, 5) and not args.graph:
         wl.W.set_option("k2_timing", 1)
         for _ in range(args.steps):
             wl.decode()
@@ -968,8 +974,8 @@ def main():
     pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes, metric)
     timed = ("HIP events at the two ends of the contract's timed region on the calls' stream / steps: " +
              STEP_KERNELS.get(kpath, KERNELS[kpath]))
-    kernel_timed = ("HIP events recorded around every ws_piece_unmask_kernel launch on the calls' stream (library "
-                    "option k2_timing), a second region of %d calls" % args.steps) if k2_ms else timed
+    kernel_timed = ("HIP events recorded around every %s launch on the calls' stream (library "
+                    "option k2_timing), a second region of %d calls" % (KERNELS[kpath], args.steps)) if k2_ms else timed
     out = {
         "metric": metric,
         "value": round(value, 2),

@@ -207,24 +207,26 @@ WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, un
 WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
- * configuration; none changes results): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse),
- * "piece_scan" (walk lanes per segment: 0 one, 1/2/3/4 64/32/16/8), "piece_whole",
- * "piece_occ", "piece_lds" (unused dynamic LDS per unmask block: caps its blocks per CU,
- * default 30000 B = 5), "piece_win" (log2 of the windows the unmask kernel streams side by side,
- * default 1), "piece_wn" / "piece_wbit" (other window maps), "seg_win" / "scan_win" /
- * "enc_win" (two windows for the segment kernels / the walk; encode 1 two windows, 2
- * XCD-contiguous), "seg_lds" / "enc_lds" (unused LDS per segment / encode copy block),
- * "segfuse_cfg", "reasm_path"
- * (0 auto, 1 fused, 2 three-kernel), "reasm_cfg", "reasm_merge", "enc_front" (encode:
- * 1 tile-scan front with the edge chunks before the copy, 0 hipcub scan and an edge
- * kernel after it), "encode_side", "encode_fused", "host_chunk_mb", "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw
- * stream: chunk-parallel walk, its largest chunk, pass rounds of a captured call), "dyn",
- * "unroll", "nt" (0 plain / 1 nontemporal loads+stores / 2 nontemporal stores),
- * "blocks_per_cu", "k2_timing" (see websocketframeGpuGetStat). Options are atomics read
- * once per call. Returns 0, or -1 for an unknown name. */
+ * configuration; every value yields bit-identical results, each one is parity-tested in
+ * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_spec"
+ * (path 3: 0 always the scan kernel + unmask, 1 adaptive — speculative, with no scan kernel,
+ * when the previous eager call on the stream advised it — 2 speculative whenever the batch
+ * fits), "spec_spins" (the speculative kernel's bounded wait for its table checkers; 0 gives
+ * up at once, exercising its repair path), "piece_lds" (unused dynamic LDS per unmask block:
+ * caps its blocks per CU; 0 = the CU's LDS / 5), "piece_win" (0..6: log2 of the windows the
+ * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
+ * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
+ * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
+ * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
+ * "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw stream: chunk-parallel walk, log2 of
+ * its largest chunk 16..26, pass rounds of a captured call 1..64), "k2_timing" (see
+ * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
+ * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
-/* Counters of the calling process's most recent call (diagnostics): "stream_rw_chunks"
+/* Counters (diagnostics): "piece_spec_calls" / "piece_classic_calls" (path-3 calls that took
+ * the speculative / the scan + unmask form, since load), "workspace_bytes" (device bytes held
+ * in workspace slots), and of the calling process's most recent call: "stream_rw_chunks"
  * (chunks of a long stream written from the chunk-parallel walk's records),
  * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront); with the option
  * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece

@@ -25,13 +25,18 @@ def dev():
     return torch.device("cuda:0")
 
 
-# decode variants: -1 auto (the default: 4 for many small segments, else 3), 3 the piece
-# path (scan kernel + one-shot 16 KiB piece unmask), 4 one workgroup per segment (segfuse)
-@pytest.fixture(params=[-1, 3, 4], ids=["auto", "piece", "segfuse"], autouse=True)
+# decode variants: -1 auto (the default: 4 for many small segments, else 3; path 3 takes the
+# speculative form when the previous call on the stream advised it), 3 the classic piece path
+# (scan kernel + one-shot 16 KiB piece unmask), 5 = path 3 forced speculative (no scan kernel,
+# ws_spec.hip), 4 one workgroup per segment (segfuse)
+@pytest.fixture(params=[(-1, 1), (3, 0), (3, 2), (4, 1)], ids=["auto", "piece", "spec", "segfuse"], autouse=True)
 def decode_path(request):
-    W.set_option("path", request.param)
-    yield request.param
+    path, spec = request.param
+    W.set_option("path", path)
+    W.set_option("piece_spec", spec)
+    yield 5 if spec == 2 else path
     W.set_option("path", -1)
+    W.set_option("piece_spec", 1)
 
 
 def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):
@@ -326,7 +331,7 @@ def test_int_truncation_real_size(dev, decode_path, total):
 
 
 @pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0),
-                                     ("piece_lds", 0), ("piece_lds", 56000)])
+                                     ("piece_lds", 1), ("piece_lds", 56000)])
 def test_window_mappings(dev, decode_path, opt, val):
     """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
     blocks store nothing), the segment kernels' two-window order (seg_win) and K2's
@@ -346,7 +351,7 @@ def test_window_mappings(dev, decode_path, opt, val):
     finally:
         W.set_option("piece_win", 1)
         W.set_option("seg_win", 1)
-        W.set_option("piece_lds", 30000)
+        W.set_option("piece_lds", 0)
 
 
 def test_cfg4_shape_vs_oracle(dev, decode_path):

@@ -16,34 +16,24 @@
 #include <atomic>
 #include <deque>
 #include <mutex>
+#include <vector>
 
 #include "ws_common.h"
 
 static __thread char g_last_error[256];
 extern std::atomic<size_t> ws_host_chunk_bytes;
-extern WsOpt ws_piece_scan;
 extern WsOpt ws_reasm_path;
 extern WsOpt ws_reasm_cfg;
-extern WsOpt ws_segfuse_cfg;
-extern WsOpt ws_enc_lds;
-extern WsOpt ws_encode_side;
-extern WsOpt ws_encode_fused;
-extern WsOpt ws_piece_whole;
-extern WsOpt ws_piece_occ;
 extern WsOpt ws_piece_lds;
 extern WsOpt ws_piece_win;
-extern WsOpt ws_piece_wbit;
 extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
-extern WsOpt ws_scan_win;
-extern WsOpt ws_piece_wn;
-extern WsOpt ws_enc_win;
 extern WsOpt ws_enc_front;
-extern WsOpt ws_seg_lds;
+extern WsOpt ws_spec_spins;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
-extern WsOpt ws_reasm_merge;
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
+size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
 int ws_set_err(const char* what, hipError_t e) {
@@ -59,66 +49,76 @@ int ws_set_msg(const char* msg) {
 extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { return g_last_error; }
 
 // ---------------------------------------------------------------------------------------------
-// launch configuration (tunable for in-process A/B by bench/profiling tools)
+// launch configuration (tunable for in-process A/B by bench/profiling tools; every value is
+// parity-tested, tests/test_gpu_options.py)
 
-struct WsTuning {
-    int path = -1;          // -1 auto (4 for many small segments, else 3), 1: walker (one wave per segment),
-                            // 3: walk + one-shot 16 KiB pieces (ws_piece), 4: one workgroup per segment,
-                            // walk + unmask fused (ws_segfuse)
-    int nt = 1;             // 0 plain, 1 nontemporal loads+stores, 2 nontemporal stores only
-    int dyn = 0;            // walker: 1 dynamic segment dequeue, 0 static grid-stride
-    int unroll = 4;         // walker: 16-B chunks per lane per batch
-    int blocks_per_cu = 64; // walker: grid cap in blocks per CU (64: one segment per wave)
-};
-static WsOpt g_path{-1}, g_nt{1}, g_dyn{0}, g_unroll{4}, g_bpc{64};
-static WsTuning tuning() {                        // one consistent read per call
-    WsTuning t;
-    t.path = g_path; t.nt = g_nt; t.dyn = g_dyn; t.unroll = g_unroll; t.blocks_per_cu = g_bpc;
-    return t;
-}
+static WsOpt g_path{-1};   // "path": -1 auto (4 for many small segments, else 3), 1 walker (one wave per
+                           // segment), 3 piece (K1 + K2, or the speculative S1 + S2), 4 segfuse
+WsOpt ws_piece_spec{1};    // "piece_spec": 0 never speculative, 1 adaptive (the device's advice from the
+                           // previous call on the slot), 2 speculative whenever the batch fits
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
     if (!strcmp(name, "path")) {
         if (value != -1 && value != 1 && value != 3 && value != 4) return -1;
         g_path = (int)value;
     }
-    else if (!strcmp(name, "nt")) g_nt = (int)value;
-    else if (!strcmp(name, "dyn")) g_dyn = (int)value;
-    else if (!strcmp(name, "unroll")) {
-        if (value != 2 && value != 4 && value != 8) return -1;
-        g_unroll = (int)value;
+    else if (!strcmp(name, "piece_spec")) {
+        if (value < 0 || value > 2) return -1;
+        ws_piece_spec = (int)value;
     }
-    else if (!strcmp(name, "blocks_per_cu")) g_bpc = (int)value;
-    else if (!strcmp(name, "host_chunk_mb") && value > 0) ws_host_chunk_bytes = (size_t)value << 20;
-    else if (!strcmp(name, "piece_scan")) ws_piece_scan = (int)value;
-    else if (!strcmp(name, "reasm_path")) ws_reasm_path = (int)value;
-    else if (!strcmp(name, "reasm_cfg")) ws_reasm_cfg = (int)value;
-    else if (!strcmp(name, "segfuse_cfg")) ws_segfuse_cfg = (int)value;
-    else if (!strcmp(name, "encode_side")) ws_encode_side = (int)value;
-    else if (!strcmp(name, "encode_fused")) ws_encode_fused = (int)value;
-    else if (!strcmp(name, "piece_whole")) ws_piece_whole = (int)value;
-    else if (!strcmp(name, "piece_occ")) ws_piece_occ = (int)value;
-    else if (!strcmp(name, "piece_lds")) ws_piece_lds = (int)value;
-    else if (!strcmp(name, "piece_win")) ws_piece_win = (int)value;
-    else if (!strcmp(name, "seg_win")) ws_seg_win = (int)value;
-    else if (!strcmp(name, "seg_lds")) ws_seg_lds = (int)value;
-    else if (!strcmp(name, "piece_wbit")) ws_piece_wbit = (int)value;
-    else if (!strcmp(name, "scan_win")) ws_scan_win = (int)value;
-    else if (!strcmp(name, "piece_wn")) ws_piece_wn = (int)value;
-    else if (!strcmp(name, "enc_win")) ws_enc_win = (int)value;
-    else if (!strcmp(name, "enc_lds")) ws_enc_lds = (int)value;
-    else if (!strcmp(name, "enc_front")) ws_enc_front = (int)value;
+    else if (!strcmp(name, "host_chunk_mb")) {
+        if (value <= 0 || value > 65536) return -1;
+        ws_host_chunk_bytes = (size_t)value << 20;
+    }
+    else if (!strcmp(name, "piece_lds")) {
+        if (value < 0 || value > 65536) return -1;
+        ws_piece_lds = (int)value;
+    }
+    else if (!strcmp(name, "piece_win")) {
+        if (value < 0 || value > 6) return -1;
+        ws_piece_win = (int)value;
+    }
+    else if (!strcmp(name, "seg_win")) {
+        if (value < 0 || value > 1) return -1;
+        ws_seg_win = (int)value;
+    }
+    else if (!strcmp(name, "reasm_path")) {
+        if (value < 0 || value > 2) return -1;
+        ws_reasm_path = (int)value;
+    }
+    else if (!strcmp(name, "reasm_cfg")) {
+        if (value < 0 || value > 2) return -1;
+        ws_reasm_cfg = (int)value;
+    }
+    else if (!strcmp(name, "enc_front")) {
+        if (value < 0 || value > 1) return -1;
+        ws_enc_front = (int)value;
+    }
+    else if (!strcmp(name, "stream_rw")) {
+        if (value < 0 || value > 1) return -1;
+        ws_stream_rw = (int)value;
+    }
+    else if (!strcmp(name, "stream_rw_cmax")) {
+        if (value < 16 || value > 26) return -1;
+        ws_stream_rw_cmax = (int)value;
+    }
+    else if (!strcmp(name, "stream_rounds")) {
+        if (value < 1 || value > 64) return -1;
+        ws_stream_rounds = (int)value;
+    }
+    else if (!strcmp(name, "spec_spins")) {
+        if (value < 0 || value > (1 << 20)) return -1;
+        ws_spec_spins = (int)value;
+    }
     else if (!strcmp(name, "k2_timing")) {
-        ws_k2_timing = (int)value;
+        ws_k2_timing = value ? 1 : 0;
         ws_k2_timing_reset();
     }
-    else if (!strcmp(name, "reasm_merge")) ws_reasm_merge = (int)value;
-    else if (!strcmp(name, "stream_rw")) ws_stream_rw = (int)value;
-    else if (!strcmp(name, "stream_rw_cmax")) ws_stream_rw_cmax = (int)value;
-    else if (!strcmp(name, "stream_rounds")) ws_stream_rounds = (int)value;
     else return -1;
     return 0;
 }
+
+extern std::atomic<unsigned long long> ws_stat_spec_calls, ws_stat_classic_calls;
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value) {
     if (!value) return -1;
@@ -130,22 +130,30 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     }
     if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks.load();
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
+    else if (!strcmp(name, "piece_spec_calls")) *value = ws_stat_spec_calls.load();
+    else if (!strcmp(name, "piece_classic_calls")) *value = ws_stat_classic_calls.load();
+    else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
     else return -1;
     return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-device state: CU count, the walker's dequeue-counter ring, and one workspace set
-// (decode + encode) per HIP stream, grown on demand. Calls on different streams of one
-// device may overlap in time (a reactor with several rx batches in flight, one stream
-// each); calls on one stream are ordered by the stream (slot rules: stream_slot).
+// Per-device state: CU count, LDS per CU, and one workspace slot per (HIP stream, graph
+// capture), grown on demand. Calls on different streams of one device may overlap in time (a
+// reactor with several rx batches in flight, one stream each); calls on one stream are ordered
+// by the stream. A call pins its slot for its whole duration (WsSlot): LRU eviction never
+// takes a pinned slot. A graph capture's slot belongs to that graph: a HIP user object on the
+// graph marks it dead when the graph (and every executable made from it) is destroyed, and the
+// next library call frees its buffers.
 #define WS_MAX_DEV 64
-#define WS_CTR_RING 64
 #define WS_STREAM_SLOTS 16
 struct WsStreamWs {
     hipStream_t stream = nullptr;
     unsigned long long capture = 0; // capture id of the graph this slot belongs to (0: eager calls)
-    bool captured = false;         // belongs to a graph capture: never reassigned, never given to eager calls
+    bool used = false;             // assigned to a stream (eager) or a capture
+    bool captured = false;         // belongs to a graph capture: never reassigned while its graph lives
+    std::atomic<int> dead{0};      // its graph was destroyed (set by the user object's destructor)
+    int busy = 0;                  // calls holding the slot (WsSlot)
     unsigned long long last = 0;   // LRU tick
     u32* ws = nullptr;             // decode / reassembly / stream workspace
     size_t ws_bytes = 0;
@@ -157,17 +165,33 @@ struct WsStreamWs {
     void* hws_dev = nullptr;       // (its device address)
     size_t hws_bytes = 0;
     bool aux_state_ok = false;     // the stream path's state (aux head) rests at zero
+    unsigned char* sws = nullptr;  // speculative piece path state (ws_spec.hip)
+    size_t sws_bytes = 0;
+    u32 spec_zero_nseg = 0;        // flags [0, this) rest at zero
+    u32 spec_parity = 0, spec_tag = 0;
+    bool spec_dirty = false;       // a call stopped between its two launches: heads not reset
+    int* adv_h = nullptr;          // pinned host word: the device's advice for the next path choice
+    int* adv_d = nullptr;
+    std::vector<void*> retired;    // buffers replaced while capturing (the graph still uses them)
 };
 struct WsDevState {
     int init = 0;
     int cus = 0;
-    u32* ctr = nullptr;
-    std::atomic<unsigned> slot{0};
+    int lds = 0;
     std::deque<WsStreamWs> sw;     // grows; stable addresses
     unsigned long long tick = 0;
 };
 static WsDevState g_dev[WS_MAX_DEV];
 static std::mutex g_dev_mu;        // device init and the stream-slot table
+std::atomic<unsigned long long> ws_stat_spec_calls{0}, ws_stat_classic_calls{0};
+
+size_t ws_workspace_bytes_total() {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    size_t t = 0;
+    for (auto& d : g_dev)
+        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes + w.sws_bytes;
+    return t;
+}
 
 static int dev_state(WsDevState** out) {
     int dev = 0;
@@ -180,21 +204,19 @@ static int dev_state(WsDevState** out) {
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return ws_set_err("hipGetDeviceProperties", e);
         st.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-        // the first call may come while the thread's stream captures a graph: allocate in
-        // relaxed mode and clear on a private non-blocking stream (neither is part of the graph)
-        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-        (void)hipThreadExchangeStreamCaptureMode(&mode);
-        hipStream_t ps = nullptr;
-        e = hipMalloc(&st.ctr, WS_CTR_RING * 128);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMemsetAsync(st.ctr, 0, WS_CTR_RING * 128, ps);
-        if (e == hipSuccess) e = hipStreamSynchronize(ps);
-        if (ps) (void)hipStreamDestroy(ps);
-        (void)hipThreadExchangeStreamCaptureMode(&mode);
-        if (e != hipSuccess) return ws_set_err("counters", e);
+        st.lds = prop.maxSharedMemoryPerMultiProcessor > 0 ? (int)prop.maxSharedMemoryPerMultiProcessor : 65536;
         st.init = 1;
     }
     *out = &st;
+    return 0;
+}
+
+int ws_device_info(int* cus, int* lds_per_cu) {
+    WsDevState* ds = nullptr;
+    const int rc = dev_state(&ds);
+    if (rc) return rc;
+    *cus = ds->cus;
+    *lds_per_cu = ds->lds;
     return 0;
 }
 
@@ -203,59 +225,115 @@ static bool capturing(hipStream_t stream) {
     return hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
 }
 
-// the id of the capture the stream is in (0: not capturing)
-static unsigned long long capture_id(hipStream_t stream) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    unsigned long long id = 0;
-    if (hipStreamGetCaptureInfo(stream, &st, &id) != hipSuccess || st != hipStreamCaptureStatusActive) return 0;
-    return id ? id : ~0ull;
+// free a slot's buffers (its stream's work, or its graph, is done)
+static void slot_free(WsStreamWs& w) {
+    (void)hipFree(w.ws);
+    (void)hipFree(w.ews);
+    (void)hipFree(w.aws);
+    (void)hipFree(w.sws);
+    if (w.hws) (void)hipHostFree(w.hws);
+    if (w.adv_h) (void)hipHostFree(w.adv_h);
+    for (void* p : w.retired) (void)hipFree(p);
+    w.retired.clear();
+    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.sws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
+    w.adv_h = nullptr; w.adv_d = nullptr;
+    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.sws_bytes = w.hws_bytes = 0;
+    w.aux_state_ok = false;
+    w.spec_zero_nseg = 0;
+    w.spec_parity = 0;
+    w.spec_dirty = false;
+    w.stream = nullptr;
+    w.capture = 0;
+    w.used = false;
+    w.captured = false;
+    w.dead = 0;
 }
 
-// the workspace slot of (stream, capture) (caller holds g_dev_mu). Eager calls keep at most
-// WS_STREAM_SLOTS slots: a further stream takes the least recently used one after a device
-// synchronize. Every graph capture gets slots of its own, keyed by its capture id (torch
-// captures every graph on one shared stream, so the stream alone does not tell graphs apart):
-// its graph uses that workspace on every replay, so it is never handed to another capture or
-// to an eager call, and graphs captured separately may be replayed concurrently.
+static void capture_slot_destroyed(void* p) { reinterpret_cast<WsStreamWs*>(p)->dead.store(1); }
+
+// the slot of (stream, capture) (caller holds g_dev_mu), pinned. Eager calls keep at most
+// WS_STREAM_SLOTS slots: a further stream takes the least recently used idle one after a
+// device synchronize (a new slot if every one is pinned). Every graph capture gets a slot of its
+// own, keyed by its capture id (torch captures every graph on one shared stream, so the stream
+// alone does not tell graphs apart): the graph uses that workspace on every replay, so it is
+// never handed to another capture or to an eager call while the graph lives.
 static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
-    const unsigned long long cap = capture_id(stream);
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    unsigned long long cap = 0;
+    hipGraph_t graph = nullptr;
+    if (hipStreamGetCaptureInfo_v2(stream, &cst, &cap, &graph, nullptr, nullptr) != hipSuccess ||
+        cst != hipStreamCaptureStatusActive)
+        cap = 0;
+    else if (!cap)
+        cap = ~0ull;
+    // release the slots of destroyed graphs
+    for (WsStreamWs& w : ds->sw)
+        if (w.used && w.captured && w.dead.load() && !w.busy) slot_free(w);
     WsStreamWs* lru = nullptr;
+    WsStreamWs* freeslot = nullptr;
+    size_t eager = 0;
     for (WsStreamWs& w : ds->sw) {
-        if (w.stream == stream && w.capture == cap) {
+        if (w.used && w.stream == stream && w.capture == cap && !w.dead.load()) {
             w.last = ++ds->tick;
+            ++w.busy;
             *out = &w;
             return 0;
         }
-        if (!w.captured && (!lru || w.last < lru->last)) lru = &w;
+        if (!w.used && !w.busy) {
+            if (!freeslot) freeslot = &w;
+            continue;
+        }
+        if (!w.captured) {
+            ++eager;
+            if (!w.busy && (!lru || w.last < lru->last)) lru = &w;
+        }
     }
-    if (cap || ds->sw.size() < WS_STREAM_SLOTS || !lru) {
+    WsStreamWs* w = nullptr;
+    if (freeslot) {
+        w = freeslot;
+    } else if (cap || eager < WS_STREAM_SLOTS || !lru) {
         ds->sw.emplace_back();
-        lru = &ds->sw.back();
-        lru->captured = cap != 0;
-    } else {                       // every slot taken by another stream: drain the device, then reuse
+        w = &ds->sw.back();
+    } else {                       // every eager slot taken by another stream: drain the device, then reuse
         hipError_t e = hipDeviceSynchronize();
         if (e != hipSuccess) return ws_set_err("hipDeviceSynchronize", e);
+        w = lru;
     }
-    lru->stream = stream;
-    lru->capture = cap;
-    lru->last = ++ds->tick;
-    *out = lru;
+    w->used = true;
+    w->stream = stream;
+    w->capture = cap;
+    w->captured = cap != 0;
+    w->last = ++ds->tick;
+    ++w->busy;
+    if (cap && graph) {
+        // tie the slot's lifetime to the graph being captured
+        hipUserObject_t uo = nullptr;
+        hipError_t e = hipUserObjectCreate(&uo, w, capture_slot_destroyed, 1, hipUserObjectNoDestructorSync);
+        if (e == hipSuccess) e = hipGraphRetainUserObject(graph, uo, 1, hipGraphUserObjectMove);
+        if (e != hipSuccess) {
+            --w->busy;
+            return ws_set_err("hipUserObjectCreate (capture workspace)", e);
+        }
+    }
+    *out = w;
     return 0;
 }
 
-// grow *p to at least `bytes` (the stream's previous work may still read it: drain first).
-// A stream capturing a graph (e.g. torch's private capture stream) may get its first
-// allocation (hipMalloc in relaxed capture mode, the head zeroed by a captured memset)
-// but cannot drain and free an existing one.
-static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, size_t zero_bytes, const char* what) {
+// grow *p to at least `bytes`. Eagerly: the stream's previous work may still read it, so drain
+// first. While capturing a graph (relaxed-mode allocation), the buffer being replaced stays
+// alive until the slot is released (kernels captured earlier in this graph use it).
+static int grow(WsStreamWs* w, void** p, size_t* have, size_t bytes, hipStream_t stream, size_t zero_bytes,
+                const char* what) {
     if (*have >= bytes) return 0;
     hipError_t e;
     const bool cap = capturing(stream);
     if (*p) {
-        if (cap) return ws_set_msg("workspace must grow while the stream captures a graph: "
-                                   "make one call of this size on the stream before capturing");
-        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
-        (void)hipFree(*p);
+        if (cap) {
+            w->retired.push_back(*p);
+        } else {
+            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
+            (void)hipFree(*p);
+        }
         *p = nullptr;
         *have = 0;
     }
@@ -283,27 +361,42 @@ static int grow(void** p, size_t* have, size_t bytes, hipStream_t stream, size_t
     return 0;
 }
 
-static int workspace(WsDevState* ds, size_t bytes, hipStream_t stream, void** out) {
+// ---- WsSlot: a (stream, capture) slot pinned for one call
+WsSlot::~WsSlot() { release(); }
+
+void WsSlot::release() {
+    if (!w) return;
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    WsStreamWs* w = nullptr;
-    int rc = stream_slot(ds, stream, &w);
-    if (rc) return rc;
-    void* p = w->ws;
-    if ((rc = grow(&p, &w->ws_bytes, bytes, stream, 16, "hipMalloc(workspace)"))) return rc;
-    w->ws = reinterpret_cast<u32*>(p);
-    *out = p;
-    return 0;
+    --w->busy;
+    w = nullptr;
 }
 
-// encode workspace (ws_encode.hip), same growth rules as the decode workspace
-int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
+int WsSlot::acquire(hipStream_t stream) {
+    release();
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    WsStreamWs* w = nullptr;
-    if ((rc = stream_slot(ds, stream, &w))) return rc;
-    if ((rc = grow(&w->ews, &w->ews_bytes, bytes, stream, 0, "hipMalloc(encode workspace)"))) return rc;
+    st = stream;
+    cus = ds->cus;
+    lds = ds->lds;
+    return stream_slot(ds, stream, &w);
+}
+
+int WsSlot::workspace(size_t bytes, size_t zero_bytes, void** out) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    void* p = w->ws;
+    const int rc = grow(w, &p, &w->ws_bytes, bytes, st, zero_bytes < 16 ? 16 : zero_bytes, "hipMalloc(workspace)");
+    w->ws = reinterpret_cast<u32*>(p);
+    if (rc) return rc;
+    *out = p;
+    return 0;
+}
+
+int WsSlot::encode_workspace(size_t bytes, void** out) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    const int rc = grow(w, &w->ews, &w->ews_bytes, bytes, st, 0, "hipMalloc(encode workspace)");
+    if (rc) return rc;
     *out = w->ews;
     return 0;
 }
@@ -311,22 +404,17 @@ int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out) {
 // auxiliary scratch (ws_stream.hip): device part grown like the workspaces, its first
 // WS_AUX_HEAD bytes zeroed at every (re)allocation (the stream path's state rests at zero);
 // a pinned, device-visible host part grown after draining the stream (never while capturing)
-int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, WsAux* out) {
-    WsDevState* ds = nullptr;
-    int rc = dev_state(&ds);
-    if (rc) return rc;
+int WsSlot::aux(size_t dbytes, size_t hbytes, WsAux* out) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    WsStreamWs* w = nullptr;
-    if ((rc = stream_slot(ds, stream, &w))) return rc;
     const void* before = w->aws;
     const size_t have = w->aws_bytes;
-    if ((rc = grow(&w->aws, &w->aws_bytes, dbytes < WS_AUX_HEAD ? WS_AUX_HEAD : dbytes, stream, WS_AUX_HEAD,
-                   "hipMalloc(aux workspace)")))
-        return rc;
+    int rc = grow(w, &w->aws, &w->aws_bytes, dbytes < WS_AUX_HEAD ? WS_AUX_HEAD : dbytes, st, WS_AUX_HEAD,
+                  "hipMalloc(aux workspace)");
+    if (rc) return rc;
     if (w->aws != before || w->aws_bytes != have) w->aux_state_ok = true;   // freshly zeroed
     if (w->hws_bytes < hbytes) {
-        if (capturing(stream)) return ws_set_msg("aux host scratch cannot grow while the stream captures a graph");
-        hipError_t e = hipStreamSynchronize(stream);
+        if (capturing(st)) return ws_set_msg("aux host scratch cannot grow while the stream captures a graph");
+        hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
         if (w->hws) (void)hipHostFree(w->hws);
         w->hws = nullptr;
@@ -347,6 +435,54 @@ int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, WsAux* ou
     return 0;
 }
 
+// the pinned advice word (eager calls only): 1 = the last call says take the speculative path
+int WsSlot::advice(int** host, int** dev) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (!w->adv_h) {
+        if (capturing(st)) return ws_set_msg("advice word cannot be allocated while capturing");
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&w->adv_h), 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return ws_set_err("hipHostMalloc(advice)", e);
+        memset(w->adv_h, 0, 64);
+        if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&w->adv_d), w->adv_h, 0)) != hipSuccess)
+            return ws_set_err("hipHostGetDevicePointer(advice)", e);
+    }
+    *host = w->adv_h;
+    *dev = w->adv_d;
+    return 0;
+}
+
+// the speculative path's state for a call over nseg segments of a span-byte range: heads +
+// flags at rest (zeroed here when needed), this call's head parity and range tag
+int WsSlot::spec(u64 span, u32 nseg, unsigned char** sws, u32* parity, u32* tag) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    const size_t need = ws_spec_workspace_bytes(span, nseg);
+    void* p = w->sws;
+    const size_t had = w->sws_bytes;
+    int rc = grow(w, &p, &w->sws_bytes, need, st, ws_spec_zero_bytes(nseg), "hipMalloc(spec workspace)");
+    w->sws = reinterpret_cast<unsigned char*>(p);
+    if (rc) return rc;
+    hipError_t e;
+    if (w->sws_bytes != had) {
+        w->spec_zero_nseg = nseg;                                   // fresh: heads + flags zeroed
+        w->spec_dirty = false;
+    }
+    if (w->spec_dirty && (e = hipMemsetAsync(w->sws, 0, 64, st)) != hipSuccess) return ws_set_err("spec reset", e);
+    w->spec_dirty = false;
+    if (nseg > w->spec_zero_nseg && (e = hipMemsetAsync(w->sws + 64, 0, (size_t)nseg * 4, st)) != hipSuccess)
+        return ws_set_err("spec flags reset", e);
+    w->spec_zero_nseg = nseg;           // flags past nseg may be overwritten by this call's list
+    *sws = w->sws;
+    *parity = w->spec_parity++;
+    w->spec_tag = (w->spec_tag + 1) & 0x7FFFFFFFu;
+    *tag = 0x80000000u | w->spec_tag;   // never a segment index (the list region) or a flag value
+    return 0;
+}
+
+void WsSlot::spec_failed() {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    w->spec_dirty = true;
+}
+
 bool ws_capturing(hipStream_t stream) { return capturing(stream); }
 
 // per-call generation number for the piece path's disorder word (never 0)
@@ -357,23 +493,15 @@ u32 ws_next_gen() {
     return gen;
 }
 
-// the calling stream's decode workspace (first 16 bytes zeroed at allocation)
-int ws_device_workspace(size_t bytes, hipStream_t stream, void** out) {
-    WsDevState* ds = nullptr;
-    int rc = dev_state(&ds);
-    if (rc) return rc;
-    return workspace(ds, bytes, stream, out);
-}
-
 // the decode variant a call takes
-static int decode_path(const WsTuning& t, u64 span, u32 nseg, u32 max_frames) {
-    if (t.path == 4) return max_frames <= 64 ? 4 : 3;                 // segfuse holds <= 64 frames per segment
-    if (t.path >= 0) return t.path;
+static int decode_path(int path, u64 span, u32 nseg, u32 max_frames) {
+    if (path == 4) return max_frames <= 64 ? 4 : 3;                   // segfuse holds <= 64 frames per segment
+    if (path >= 0) return path;
     return ws_segfuse_fits(span, nseg, max_frames) ? 4 : 3;
 }
 
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
-    const int path = decode_path(tuning(), span, nseg, max_frames);
+    const int path = decode_path(g_path, span, nseg, max_frames);
     return path == 3 ? ws_piece_workspace_bytes(span, nseg, max_frames) : 0;
 }
 
@@ -388,29 +516,48 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     WsDevState* ds = nullptr;
     int rc = dev_state(&ds);
     if (rc) return rc;
-    const WsTuning t = tuning();
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg; L.max_frames = max_frames;
     L.desc_base = d_desc_base; L.desc = d_desc; L.res = d_res;
     L.stream = stream;
     L.cus = ds->cus;
-    u32* ctr = ds->ctr + (size_t)(ds->slot++ % WS_CTR_RING) * 32;
-    const int path = decode_path(t, hi - lo, nseg, max_frames);
-    if (path == 1) return ws_launch_walker(L, t.unroll, t.nt, t.dyn, t.blocks_per_cu, ctr);
-    if (path == 4) return ws_launch_segfuse(L, t.nt);
+    L.lds_per_cu = ds->lds;
+    const int path = decode_path(g_path, hi - lo, nseg, max_frames);
+    if (path == 1) return ws_launch_walker(L);
+    if (path == 4) return ws_launch_segfuse(L);
     const size_t need = ws_decode_workspace_bytes(hi - lo, nseg, max_frames);
     if (ws && ws_bytes < need) return ws_set_msg("websocketframe batch decode: workspace too small");
-    if (!ws && need) {
-        if ((rc = workspace(ds, need, L.stream, &ws))) return rc;
+    WsSlot slot;
+    int* adv_h = nullptr;
+    int* adv_d = nullptr;
+    if (!ws) {
+        if ((rc = slot.acquire(stream))) return rc;
+        const bool cap = capturing(stream);
+        const int spec_opt = ws_piece_spec;
+        if (!cap && (rc = slot.advice(&adv_h, &adv_d))) return rc;
+        // speculative (no K1): eager calls only, when the checkers can cover the segment table,
+        // and when the device advised it after the previous call on this slot (or forced)
+        if (!cap && spec_opt && ws_spec_fits(hi - lo, nseg) &&
+            (spec_opt == 2 || __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1)) {
+            unsigned char* sws = nullptr;
+            u32 parity = 0, tag = 0;
+            if ((rc = slot.spec(hi - lo, nseg, &sws, &parity, &tag))) return rc;
+            ++ws_stat_spec_calls;
+            rc = ws_launch_piece_spec(L, lo, hi, sws, parity, tag, adv_d);
+            if (rc) slot.spec_failed();
+            return rc;
+        }
+        if (need && (rc = slot.workspace(need, 16, &ws))) return rc;
     }
+    ++ws_stat_classic_calls;
     const u32 gen = ws_next_gen();
     const u32* disorder = nullptr;
     bool fallback = false;
-    if ((rc = ws_launch_piece(L, lo, hi, t.nt, reinterpret_cast<unsigned char*>(ws), gen, &disorder, &fallback)))
+    if ((rc = ws_launch_piece(L, lo, hi, reinterpret_cast<unsigned char*>(ws), gen, adv_d, &disorder, &fallback)))
         return rc;
     // segments out of buffer order are decoded by K2's fallback; with no pieces to launch K2
     // on, a small gated walker grid does it (exits at once for ordered batches)
-    return fallback ? ws_launch_walker(L, t.unroll, t.nt, 0, 1, ctr, disorder, gen) : 0;
+    return fallback ? ws_launch_walker(L, disorder, gen) : 0;
 }
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeDevice(unsigned char* d_buf, unsigned long long buflen,

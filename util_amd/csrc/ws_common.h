@@ -346,22 +346,31 @@ struct WsLaunch {
     WebsocketSegResult_t* res;
     hipStream_t stream;
     int cus;
+    int lds_per_cu;       // bytes of LDS per CU (hipDeviceProp_t::maxSharedMemoryPerMultiProcessor)
 };
-int ws_launch_walker(const WsLaunch& L, int unroll, int nt, int dyn, int blocks_per_cu, u32* ctr,
-                     const u32* gate = nullptr, u32 gate_gen = 0);
+int ws_launch_walker(const WsLaunch& L, const u32* gate = nullptr, u32 gate_gen = 0);
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 struct PieceWs {          // ws_piece.hip workspace views after K1
     u32* disorder;
+    u32* nonuni;          // K1's count of segments with frames of several lengths (K2 reads + clears)
     u64* ptr;
     u32* nwork;           // items per segment (frames walked, incl. an unconsumed ret==0 frame)
     u32x4* items;         // per descriptor slot s*max_frames+k: P0|rk_lo<<48, P1|rk_hi<<48 (origin-relative)
     u64 npieces, pbase, c_lo, c_hi;
 };
-int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out);
+int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
+                         bool count_nonuniform = false);
+int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr);
+int ws_piece_dyn_lds(const WsLaunch& L);
+// the speculative piece path (ws_spec.hip): no K1; sws = the slot's spec workspace
+size_t ws_spec_workspace_bytes(u64 span, u32 nseg);
+size_t ws_spec_zero_bytes(u32 nseg);
+bool ws_spec_fits(u64 span, u32 nseg);
+int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, int* advice_dev);
 u32 ws_next_gen();
-int ws_device_workspace(size_t bytes, hipStream_t stream, void** out);
-// the calling stream's auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are
-// zero at allocation + pinned, device-visible host scratch (eager calls)
+int ws_device_info(int* cus, int* lds_per_cu);
+// auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are zero at allocation +
+// pinned, device-visible host scratch (eager calls)
 #define WS_AUX_HEAD 256
 struct WsAux {
     void* d;              // device scratch
@@ -369,10 +378,27 @@ struct WsAux {
     void* h_dev;          // its device address
     bool* state_ok;       // the owner's flag: the head holds a resting state
 };
-int ws_aux_workspace(size_t dbytes, size_t hbytes, hipStream_t stream, WsAux* out);
+// The workspace slot of (HIP stream, graph capture), pinned for one call (ws_api.hip): every
+// buffer a call needs comes from the one slot it acquired, and LRU eviction never takes a
+// pinned slot. Buffers grow on demand (eagerly: after draining the stream).
+struct WsStreamWs;
+struct WsSlot {
+    WsStreamWs* w = nullptr;
+    hipStream_t st = nullptr;
+    int cus = 0, lds = 0;
+    ~WsSlot();
+    int acquire(hipStream_t stream);
+    void release();
+    int workspace(size_t bytes, size_t zero_bytes, void** out);   // decode / reassembly / stream
+    int encode_workspace(size_t bytes, void** out);
+    int aux(size_t dbytes, size_t hbytes, WsAux* out);
+    int advice(int** host, int** dev);                             // the path advice word (eager)
+    int spec(u64 span, u32 nseg, unsigned char** sws, u32* parity, u32* tag);
+    void spec_failed();
+};
 bool ws_capturing(hipStream_t stream);
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
-                    bool* fallback_needed);
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,
+                    const u32** disorder_out, bool* fallback_needed);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
 // (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes whose
 // first 16 bytes were zeroed once after allocation, else the per-device one is used
@@ -381,7 +407,7 @@ int ws_decode_range(unsigned char* buf, u64 lo, u64 hi, const u64* seg_off, cons
                     u32 max_frames, const u64* desc_base, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res,
                     hipStream_t stream, void* ws = nullptr, size_t ws_bytes = 0);
 size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
-int ws_launch_segfuse(const WsLaunch& L, int nt);
+int ws_launch_segfuse(const WsLaunch& L);
 bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
 
 // Block -> work item with the items split into two windows streamed side by side

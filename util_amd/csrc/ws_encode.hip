@@ -512,39 +512,11 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front_kernel(const unsigned c
     enc_edges(src, f, n, i, e, nx, dst, min(all, capacity), enc_fused != 0);
 }
 
-int ws_encode_workspace(size_t bytes, hipStream_t stream, void** out);
 
-// per-device side stream + fork/join events for E4 (created on first use)
-#define ENC_MAX_DEV 64
-struct EncSide {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-static EncSide g_side[ENC_MAX_DEV];
-
-static int enc_side(EncSide** out) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return ws_set_err("hipGetDevice", e);
-    if (dev < 0 || dev >= ENC_MAX_DEV) return ws_set_err("device index", hipErrorInvalidDevice);
-    EncSide& S = g_side[dev];
-    if (!S.s) {
-        if ((e = hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking)) != hipSuccess) return ws_set_err("hipStreamCreate", e);
-        if ((e = hipEventCreateWithFlags(&S.fork, hipEventDisableTiming)) != hipSuccess) return ws_set_err("hipEventCreate", e);
-        if ((e = hipEventCreateWithFlags(&S.join, hipEventDisableTiming)) != hipSuccess) return ws_set_err("hipEventCreate", e);
-    }
-    *out = &S;
-    return 0;
-}
-WsOpt ws_encode_fused{0}; // "encode_fused": 1 E3 stores the edge chunks of eligible frames and E4 skips them
-                          // (measured slower: 96 VGPRs and a dependent round trip before the payload loads)
-WsOpt ws_enc_lds{0};      // "enc_lds": bytes of unused dynamic LDS per E3 block (occupancy A/B)
-WsOpt ws_enc_win{0};      // "enc_win": E3 takes output pieces in two windows (1, ws_win2; measured 1 % slower)
-                          // or XCD-contiguous (2)
+// Measured and dropped (round 2): E4 on a side stream, edges fused into E3,
+// E3 over two windows or XCD-contiguous pieces, fewer E3 blocks per CU.
 WsOpt ws_enc_front{1};    // "enc_front": 1 F1-F3 front (tile sums, tile scan, one thread per frame: offsets,
                           // piece pointers, edge chunks) before E3; 0 hipcub scan + E2, E3, then E4
-WsOpt ws_encode_side{0};  // "encode_side": 1 E4 on a side stream concurrent with E2+E3 (measured slower:
-                          // its latency-bound blocks take CU slots from E3), 0 after E3 (default)
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,
                                                                   const WebsocketEncodeDesc_t* d_frames,
@@ -557,18 +529,19 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     const u64 lead0 = reinterpret_cast<uintptr_t>(d_dst) & 15;
     const u64 npieces = (dst_capacity + lead0 + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT;
-    const bool side = ws_encode_side, front = ws_enc_front && !side;
-    const u32 fused = ws_encode_fused && npieces ? 1u : 0u;
+    const bool front = ws_enc_front != 0;
+    const u32 fused = 0u;
     hipError_t e;
     int rc;
     void* ws = nullptr;
     u32* ptr = nullptr;
-    EncSide* S = nullptr;
+    WsSlot slot;
+    if ((rc = slot.acquire(st))) return rc;
     if (front) {
         // F1 tile sums -> F2 tile scan (also wire_off[n]) -> F3 offsets, piece pointers, edges
         const u32 B = (nframes + ENC_TILE - 1) / ENC_TILE, blocks = B;
         const size_t ptr_off = ((size_t)(B + 1) * 8 + 255) & ~(size_t)255;
-        if ((rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws))) return rc;
+        if ((rc = slot.encode_workspace(ptr_off + npieces * 4 + 16, &ws))) return rc;
         u64* tpre = reinterpret_cast<u64*>(ws);
         ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
         hipLaunchKernelGGL(ws_enc_tsum_kernel, dim3(blocks), dim3(ENC_TILE), 0, st, d_frames, nframes, tpre);
@@ -585,36 +558,18 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
             return ws_set_err("hipcub scan (size)", e);
         const size_t ptr_off = (scan_bytes + 255) & ~(size_t)255;
-        if ((rc = ws_encode_workspace(ptr_off + npieces * 4 + 16, st, &ws))) return rc;
+        if ((rc = slot.encode_workspace(ptr_off + npieces * 4 + 16, &ws))) return rc;
         if ((e = hipcub::DeviceScan::ExclusiveSum(ws, scan_bytes, in, d_wire_off, nframes + 1, st)) != hipSuccess)
             return ws_set_err("hipcub scan", e);
         ptr = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(ws) + ptr_off);
-        if (side) {
-            if ((rc = enc_side(&S))) return rc;
-            if ((e = hipEventRecord(S->fork, st)) != hipSuccess) return ws_set_err("hipEventRecord", e);
-            if ((e = hipStreamWaitEvent(S->s, S->fork, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
-            hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, S->s, d_src, d_frames,
-                               nframes, d_wire_off, d_dst, (u64)dst_capacity, 0u);
-            if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_edge_kernel launch", e);
-            if ((e = hipEventRecord(S->join, S->s)) != hipSuccess) return ws_set_err("hipEventRecord", e);
-        }
         hipLaunchKernelGGL(ws_enc_ptr_kernel, dim3((nframes + 1 + 255) / 256), dim3(256), 0, st, d_frames, nframes,
                            d_wire_off, ptr, lead0, npieces);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     }
     if (npieces) {
-        auto copy = fused && !S ? ws_enc_copy_kernel<1, 1> : ws_enc_copy_kernel<1, 0>;
-        const int win = ws_enc_win;
-        const u32 half = win == 2 ? ~0u : (win == 1 && npieces >= 512 ? (u32)((npieces + 1) / 2) : 0);
-        const u32 grid = win == 2 ? (u32)(((npieces + 7) >> 3) << 3) : (half ? 2 * half : (u32)npieces);
-        const int dyn = ws_enc_lds;                                            // unused LDS: fewer blocks per CU
-        hipLaunchKernelGGL(copy, dim3(grid), dim3(ENC_T), dyn > 0 && dyn <= 65536 ? dyn : 0, st, d_src, d_frames, nframes,
-                           d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, half);
+        hipLaunchKernelGGL((ws_enc_copy_kernel<1, 0>), dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames, nframes,
+                           d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, 0u);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
-    }
-    if (S) {
-        if ((e = hipStreamWaitEvent(st, S->join, 0)) != hipSuccess) return ws_set_err("hipStreamWaitEvent", e);
-        return 0;
     }
     if (front) return 0;
     hipLaunchKernelGGL(ws_enc_edge_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, d_src, d_frames, nframes,

@@ -6,15 +6,17 @@
 // with a chain of 4 dependent table lookups resolved while their payload loads are
 // in flight (tools/calib.py modes 4, 5, 40-49, 60-65).
 //
-// K1 ws_piece_walk_kernel — one LANE per rx segment runs the reactor loop
+// K1 ws_piece_scan_kernel — 16 lanes per rx segment run the reactor loop
 //   (net_reactor.c:515-526) over websocketframeDecode's header logic
-//   (websocketframe.c:112-165, ws_parse). Writes the descriptors and segment result,
-//   one payload item per frame (origin-relative [P0, P1) + pre-rotated key, indexed
-//   like the descriptor slot s*max_frames + k), the item count per segment, and for
-//   every 16 KiB piece whose first byte lies in this segment's ownership range
-//   [end of segment s-1, end of segment s) the first item that can touch it.
-//   A segment that starts before the previous one ends (or lies outside [lo, hi))
-//   marks the batch unordered.
+//   (websocketframe.c:112-165, ws_parse) by stride speculation. Writes the descriptors
+//   and segment result, one payload item per frame (origin-relative [P0, P1) +
+//   pre-rotated key, indexed like the descriptor slot s*max_frames + k), the item count
+//   per segment, and for every 16 KiB piece whose first byte lies in this segment's
+//   ownership range [end of segment s-1, end of segment s) the first item that can touch
+//   it. A segment that starts before the previous one ends (or lies outside [lo, hi))
+//   marks the batch unordered. It also counts the segments whose frames are not all of
+//   the first frame's length (or that stop on an error): K2 turns that count into the
+//   host's advice to take the speculative path (ws_spec.hip, no K1) on the next call.
 // K2 ws_piece_unmask_kernel — one 256-thread block per piece, 4 chunks per lane:
 //   payload loads first, then (while they are in flight) the piece pointer and the
 //   items it leads to (16, then 64 per load, hopping to the next segment when the piece
@@ -33,7 +35,6 @@
 #define PIECE_SHIFT WS_PIECE_SHIFT
 static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's chunks");
 #define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
-#define PWALK_T 256
 
 // item: w0 = P0 | rkey[15:0] << 48, w1 = P1 | rkey[31:16] << 48 (origin-relative bytes < 2^48)
 __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
@@ -51,74 +52,12 @@ __device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 pend, u64 lo, 
     for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi && p < pend; ++p) *gptr<u64>(ptr + (p - pbase)) = val;
 }
 
-__global__ __launch_bounds__(PWALK_T) void ws_piece_walk_kernel(const unsigned char* __restrict__ buf,
-                                                                 const u64* __restrict__ seg_off,
-                                                                 const u64* __restrict__ seg_len, u32 nseg,
-                                                                 u32 max_frames, const u64* __restrict__ desc_base,
-                                                                 WebsocketFrameDesc_t* __restrict__ desc,
-                                                                 WebsocketSegResult_t* __restrict__ res,
-                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
-                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
-                                                                 u32 gen, u64 pbase, u64 lo, u64 hi) {
-    const u32 s = blockIdx.x * PWALK_T + threadIdx.x;
-    if (s >= nseg) return;
-    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
-    const u64 pend = hi + lead0 ? ((hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
-    const u64 so = seg_off[s], sl = seg_len[s];
-    const u64 prev_end = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
-    // out of order, or outside the declared range: the gated walker decodes the batch instead
-    if (prev_end > so || so < lo || so > hi || sl > hi - so) *gptr<u32>(disorder) = gen;
-    const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
-    const u64 ibase = (u64)s * max_frames;
-    const u64 sorg = so + lead0;                                            // origin-relative segment start
-    const u64 tag = (u64)s << 32;
-    put_ptrs(ptr, pbase, pend, s ? prev_end + lead0 : 0, sorg, tag);                     // pieces starting in the gap before s
-    u64 off = 0, walked_end = sorg;
-    u32 nf = 0, extra = 0;
-    int status = WEBSOCKET_SEG_OK;
-    uintptr_t p = reinterpret_cast<uintptr_t>(buf + so);
-    u32x4 x0 = reinterpret_cast<const gu32x4*>(p & ~(uintptr_t)15)[0];
-    u32x4 x1 = reinterpret_cast<const gu32x4*>(p & ~(uintptr_t)15)[1];
-    while (off < sl) {
-        if (nf >= max_frames) { status = WEBSOCKET_SEG_MAX_FRAMES; break; }
-        const u64 avail = sl - off;
-        if (avail < 2) break;                                                // websocketframe.c:121
-        u64 h0, h1;
-        ws_hdr_from32(x0, x1, (u32)(p & 15), h0, h1);
-        const WsHdr h = ws_parse(h0, h1, avail);
-        if (h.kind == WS_PARSE_INCOMPLETE) break;
-        if (h.kind == WS_PARSE_WRAP) { status = WEBSOCKET_SEG_ERR_LEN_WRAP; break; }
-        // next header's loads issue before this frame's stores (vmcnt retires in order)
-        const uintptr_t pn = h.ret > 0 && off + (u32)h.ret < sl ? p + (u32)h.ret : p;
-        const gu32x4* qn = reinterpret_cast<const gu32x4*>(pn & ~(uintptr_t)15);
-        x0 = qn[0];
-        x1 = qn[1];
-        const u64 fo = sorg + off;                                           // frame start (origin-relative)
-        const u64 p0 = fo + h.hdr;
-        walked_end = p0 + h.plen;                                            // frame extent (ret may truncate)
-        // item k = nf: the payload range if masked, else an empty range at the payload start
-        put_item(gptr<u32x4>(items + ibase + nf), p0, h.masked ? walked_end : p0, rotl32(h.key, 8u * (u32)(p0 & 3)));
-        put_ptrs(ptr, pbase, pend, fo, walked_end, tag | nf);                             // pieces starting inside this frame
-        if (h.ret == 0) { extra = 1; break; }                                // (int) truncated to 0: unmasked,
-        ws_store_desc(desc + dbase + nf, so + off, h);                       // no descriptor, loop breaks
-        ++nf;
-        if (h.ret < 0) { status = WEBSOCKET_SEG_ERR_DECODE; break; }         // net_reactor.c:518-520
-        off += (u32)h.ret;                                                   // net_reactor.c:525
-        p = pn;
-    }
-    const u32 cnt = nf + extra;
-    put_ptrs(ptr, pbase, pend, walked_end, sorg + sl, tag | cnt);                         // pieces starting in the tail
-    if (s == nseg - 1) put_ptrs(ptr, pbase, pend, sorg + sl, hi + lead0, PIECE_NONE);      // after the last segment
-    ws_store_res(res + s, off, nf, status);
-    *gptr<u32>(nwork + s) = cnt;
-}
-
-// K1, group variant: G lanes (16/32/64) per segment, header walk by STRIDE SPECULATION
-// (as ws_segblock.hip): lane k of the group parses the header at off + k*g (g = the
-// last frame's length); the chain is right up to the first lane whose frame length
-// differs (ballot), so a run of up to G equal frames is walked in one round trip and
-// its items, descriptors and piece pointers are written by the lanes in parallel.
-// Small G keeps more segments in flight per wave (the walk is latency-bound).
+// K1: G = 16 lanes per segment, header walk by STRIDE SPECULATION: lane k of the group
+// parses the header at off + k*g (g = the last frame's length); the chain is right up
+// to the first lane whose frame length differs (ballot), so a run of up to G equal frames
+// is walked in one round trip and its items, descriptors and piece pointers are written
+// by the lanes in parallel. 16 keeps four segments in flight per wave (the walk is
+// latency-bound; 8, 32, 64 lanes and one lane per segment measured slower in round 1).
 #define PSCAN_T 256
 template <int G>
 __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned char* __restrict__ buf,
@@ -129,11 +68,11 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 WebsocketSegResult_t* __restrict__ res,
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
-                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32 half) {
-    static_assert(G == 8 || G == 16 || G == 32 || G == 64, "group size");
+                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32* nonuni) {
+    static_assert(G == 16, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
-    const u32 s = (ws_win2(blockIdx.x, half) * PSCAN_T + threadIdx.x) / G;  // half > 0: two windows
+    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / G;
     bool active = s < nseg;
     const u32 sc = active ? s : nseg - 1;                                    // inactive groups: harmless loads
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
@@ -150,6 +89,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     u64 off = 0, g = 0, walked_end = sorg;
     u32 nf = 0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
+    bool nonu = false;                       // frames of another length than the first, or an error stop
     const u64 gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
     while (__ballot(active)) {
         const u64 pos = off + (u64)gl * g;                                  // candidate frame offset
@@ -200,6 +140,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         const u64 pos_m = off + (u64)mm * g;
         nf += mm;
         if (code_m == 1) {                                                  // consumed, new stride
+            if (nf) nonu = true;
             nf += 1;
             off = pos_m + (u32)ret_m;
             g = (u32)ret_m;
@@ -209,8 +150,10 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         if (code_m == 2) {
             if (ret_m != 0) nf += 1;                                        // ret < 0 keeps its descriptor
             else extra = 1;                                                 // ret == 0: unmasked, not counted
+            nonu = true;
         }
         status = st_m;
+        if (st_m == WEBSOCKET_SEG_ERR_LEN_WRAP) nonu = true;
         active = false;
         if (gl == 0) {
             const u32 cnt = nf + extra;
@@ -220,10 +163,18 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
             *gptr<u32>(nwork + s) = cnt;
         }
     }
+    if (nonuni) {                                                           // one atomic per wave, if any
+        const u64 b = __ballot(gl == 0 && s < nseg && nonu);
+        if (lane == 0 && b) atomicAdd(nonuni, (u32)__popcll(b));
+    }
 }
 
-template <int NT, u32 WHOLE, int OCC>
-__global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
+// K2. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
+// exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
+// all measured slower): nontemporal loads and stores, chunks wholly inside
+// segments stored whole (byte coverage by the visited segments), 2^wshift windows.
+template <int NT>
+__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
                                                                   const u64* __restrict__ seg_len, u32 nseg,
                                                                   u32 max_frames, const u32x4* __restrict__ items,
@@ -233,18 +184,15 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
                                                                   u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
                                                                   WebsocketSegResult_t* __restrict__ res,
-                                                                  u32 wshift, u32 wbit, u64 ppw, u64 npieces, u32 wn) {
+                                                                  u32 wshift, u64 ppw, u64 npieces, u32* nonuni,
+                                                                  int* advice) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
-    // (window index from block bits [wbit, wbit + wshift); ppw is a multiple of 2^wbit)
     const u32 bx = blockIdx.x;
-    // (wn > 0: wn windows of any count, block b -> (b mod wn) * ppw + b / wn)
-    const u64 pw = wn ? (u64)(bx % wn) * ppw + bx / wn
-                      : (u64)((bx >> wbit) & ((1u << wshift) - 1u)) * ppw +
-                            (((bx >> (wbit + wshift)) << wbit) | (bx & ((1u << wbit) - 1u)));
+    const u64 pw = (u64)(bx & ((1u << wshift) - 1u)) * ppw + (bx >> wshift);
     const bool pvalid = pw < npieces;
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
@@ -283,16 +231,14 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
     // (bytes the decode does not change are written back unchanged: one 16-B store
-    // instead of byte stores); others get exact byte stores. WHOLE 1: a bit per chunk
-    // inside ONE visited segment (72 VGPRs); WHOLE 2: byte coverage by the visited
-    // segments, so chunks spanning two adjacent segments count too (80 VGPRs).
-    u32 whole = 0;
+    // instead of byte stores; byte coverage by the visited segments, so chunks spanning
+    // two adjacent segments count too); others get exact byte stores.
     u32 segcov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) segcov[u] = 0;
     while (s < nseg) {
         const u32 cnt = nwork[s];
-        if (WHOLE) {
+        {
             // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
             const long long sa = (long long)(seg_off[s] + lead0 - r0), sb = sa + (long long)seg_len[s];
             const int SA = (int)(sa < -16 ? -16 : (sa > RW + 16 ? RW + 16 : sa));
@@ -300,13 +246,9 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
 #pragma unroll
             for (int u = 0; u < PIECE_U; ++u) {
                 const int x = u * 1024 + xl;
-                if constexpr (WHOLE == 1) {
-                    whole |= (x >= SA && x + 16 <= SB) ? (1u << u) : 0u;
-                } else {
-                    const int lo = SA > x ? (SA - x < 16 ? SA - x : 16) : 0;
-                    const int hi = SB > x ? (SB - x < 16 ? SB - x : 16) : 0;
-                    if (hi > lo) segcov[u] |= (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
-                }
+                const int lo = SA > x ? (SA - x < 16 ? SA - x : 16) : 0;
+                const int hi = SB > x ? (SB - x < 16 ? SB - x : 16) : 0;
+                if (hi > lo) segcov[u] |= (0xFFFFu >> (16 - hi)) & (0xFFFFu << lo);
             }
         }
         if (k < cnt) {
@@ -356,7 +298,7 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
         const u64 c = wc0 + (u64)(u * 64 + lane);
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         const u32x4 w = v[u];
-        if (cov[u] == 0xFFFFu || (WHOLE == 1 && ((whole >> u) & 1u)) || (WHOLE == 2 && segcov[u] == 0xFFFFu)) {
+        if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
             st16<NT>(w, base + c);
         } else {
             ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
@@ -368,12 +310,20 @@ __global__ __launch_bounds__(PIECE_T) __attribute__((amdgpu_waves_per_eu(OCC, 8)
         for (u32 s2 = blockIdx.x * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
             walk_segment<4, NT>(buf, s2, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
     }
+    // the host's next path choice (ws_api.hip): speculative while at most 1/32 of the
+    // segments had frames of more than one length (K1 has finished: its count is final)
+    if (advice && bx == 0 && tid == 0) {
+        const u32 n = *gptr<u32>(nonuni);
+        *gptr<u32>(nonuni) = 0;
+        __hip_atomic_store(advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-// ws layout: [disorder u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
+// ws layout: [disorder u32 | nonuni u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
 // No per-call reset: K1 writes every piece pointer, and marks an unordered batch by
 // storing this call's generation number `gen` (never 0) into `disorder`, which the
-// workspace owner zeroes once when it allocates the workspace.
+// workspace owner zeroes once when it allocates the workspace. `nonuni` (K1's count of
+// segments with frames of several lengths) rests at zero: K2 reads and clears it.
 static u64 piece_count(u64 lo_org, u64 hi_org) {
     return hi_org > lo_org ? ((hi_org - 1) >> PIECE_SHIFT) - (lo_org >> PIECE_SHIFT) + 1 : 0;
 }
@@ -385,14 +335,11 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     return b + (size_t)nseg * max_frames * 16 + 16;
 }
 
-// Segments lie in [lo, hi) of L.buf. Launches K1 and K2; *disorder_out = the word a gated
-// fallback walker compares with `gen`.
-WsOpt ws_piece_scan{3};  // K1 variant ("piece_scan"): 0 one lane per segment, 1/2/3/4: 64/32/16/8 lanes per segment
-
-// K1 alone (also the first stage of the reassembly path, ws_reasm.hip)
-WsOpt ws_scan_win{0};    // "scan_win": K1 takes its segment groups in two windows (ws_win2)
-
-int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out) {
+// K1 alone (also the first stage of the reassembly path, ws_reasm.hip). Segments lie in
+// [lo, hi) of L.buf. count_nonuniform: K1 counts segments with frames of several lengths
+// for the K2 that follows (ws_launch_piece); other users pass false.
+int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
+                         bool count_nonuniform) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     PieceWs P;
@@ -401,49 +348,41 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     P.c_lo = lo_org >> 4;
     P.c_hi = (hi_org + 15) >> 4;
     P.disorder = reinterpret_cast<u32*>(ws);
+    P.nonuni = reinterpret_cast<u32*>(ws) + 1;
     P.ptr = reinterpret_cast<u64*>(ws + 16);
     size_t b = (16 + P.npieces * 8 + 15) & ~(size_t)15;
     P.nwork = reinterpret_cast<u32*>(ws + b);
     b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
     P.items = reinterpret_cast<u32x4*>(ws + b);
-    const int scan = ws_piece_scan;
-    if (scan >= 1 && scan <= 4) {
-        const int G = scan == 1 ? 64 : (scan == 2 ? 32 : (scan == 3 ? 16 : 8));
-        const u32 blocks = (u32)(((u64)L.nseg * G + PSCAN_T - 1) / PSCAN_T);
-        const u32 half = ws_scan_win && blocks >= 512 ? (blocks + 1) / 2 : 0;
-        auto k = G == 64 ? ws_piece_scan_kernel<64>
-                         : (G == 32 ? ws_piece_scan_kernel<32> : (G == 16 ? ws_piece_scan_kernel<16> : ws_piece_scan_kernel<8>));
-        hipLaunchKernelGGL(k, dim3(half ? 2 * half : blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
-                           L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
-                           P.disorder, gen, P.pbase, lo, hi, half);
-    } else {
-        hipLaunchKernelGGL(ws_piece_walk_kernel, dim3((L.nseg + PWALK_T - 1) / PWALK_T), dim3(PWALK_T), 0, L.stream,
-                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items,
-                           P.nwork, P.ptr, P.disorder, gen, P.pbase, lo, hi);
-    }
+    const u32 blocks = (u32)(((u64)L.nseg * 16 + PSCAN_T - 1) / PSCAN_T);
+    hipLaunchKernelGGL(ws_piece_scan_kernel<16>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
+                       L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
+                       P.disorder, gen, P.pbase, lo, hi, count_nonuniform ? P.nonuni : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
     *out = P;
     return 0;
 }
 
-// K2 alone over the pieces of a scanned batch
-WsOpt ws_piece_whole{2}; // "piece_whole": 2 whole stores for chunks inside segments (default), 1 only inside
-                          // one segment, 0 exact bytes only
-// "piece_lds": bytes of unused dynamic LDS per K2 block, which caps K2's blocks (= waves per
-// SIMD) per CU at 160 KiB / bytes: 30000 -> 5. K2 needs only 58 VGPRs (8 waves/SIMD would
-// fit) but streams best at 5: cfg2 1.363-1.366 ms at 5 against 1.378-1.382 (6), 1.395-1.399
-// (7), 1.402-1.420 (8), 1.386-1.387 (4); cfg3 and cfg4 the same way (profiles/r02_k2_occupancy_ab.log)
-WsOpt ws_piece_lds{30000};
-WsOpt ws_piece_occ{0};   // "piece_occ": minimum waves/SIMD the compiler must fit K2 in (0/1: its choice, 7, 8)
-WsOpt ws_piece_wn{0};    // "piece_wn": >= 2 windows of any count (overrides piece_win/piece_wbit)
-WsOpt ws_piece_wbit{0};  // "piece_wbit": block-index bit that selects the window (0: alternate blocks)
+// "piece_lds": bytes of unused dynamic LDS per K2 (and speculative S1) block, which caps its
+// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 5 — K2 needs only 58 VGPRs
+// (8 waves/SIMD would fit) but streams best at 5 blocks per CU: cfg2 1.363-1.366 ms at 5
+// against 1.378-1.382 (6), 1.395-1.399 (7), 1.402-1.420 (8), 1.386-1.387 (4); cfg3 and cfg4
+// the same way (profiles/r02_k2_occupancy_ab.log). On gfx950 (160 KiB per CU) that is 32 KiB.
+WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
+int ws_piece_dyn_lds(const WsLaunch& L) {
+    const int opt = ws_piece_lds;
+    if (opt > 0) return opt <= 65536 ? opt : 65536;
+    const int per = L.lds_per_cu / 5;                       // 5 blocks per CU
+    return per > 65536 ? 65536 : (per & ~255);
+}
+
 // "k2_timing" (measurement only, bench.py): a pair of HIP events is recorded around every
-// K2 launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
-// recorded K2 durations, "k2_calls" counts them; setting the option clears the record.
+// K2 (or S1) launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
+// recorded durations, "k2_calls" counts them; setting the option clears the record.
 WsOpt ws_k2_timing{0};
 static std::vector<hipEvent_t> g_k2ev;    // start, end, start, end, ...
 static size_t g_k2n = 0;
@@ -469,7 +408,7 @@ int ws_k2_stat(unsigned long long* ns, unsigned long long* calls) {
     return 0;
 }
 
-static int k2_mark(hipStream_t st, bool end, size_t* slot) {
+int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
     std::lock_guard<std::mutex> lk(g_k2mu);
     if (!end) *slot = g_k2n++;
     const size_t i = 2 * *slot + (end ? 1 : 0);
@@ -483,43 +422,34 @@ static int k2_mark(hipStream_t st, bool end, size_t* slot) {
     return 0;
 }
 
-int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen) {
+// K2 over the pieces of a scanned batch; advice (device view of pinned host memory, may be
+// null): K2 turns K1's non-uniform count into the host's next path choice
+int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice) {
     if (!P.npieces) return 0;
     size_t tslot = 0;
     int rc;
-    const int timing = ws_k2_timing, whole = ws_piece_whole, occ = ws_piece_occ;
-    const int pwin = ws_piece_win, pwbit = ws_piece_wbit, pwn = ws_piece_wn;
-    if (timing && (rc = k2_mark(L.stream, false, &tslot))) return rc;
-    auto k = nt == 1 ? (whole == 2 ? ws_piece_unmask_kernel<1, 2, 1>
-                                   : (whole == 1 ? ws_piece_unmask_kernel<1, 1, 1> : ws_piece_unmask_kernel<1, 0, 1>))
-                     : (whole == 2 ? ws_piece_unmask_kernel<0, 2, 1>
-                                   : (whole == 1 ? ws_piece_unmask_kernel<0, 1, 1> : ws_piece_unmask_kernel<0, 0, 1>));
-    if (occ == 7 || occ == 8)                              // forced occupancy: spills, measured slower
-        k = occ == 8 ? ws_piece_unmask_kernel<1, 1, 8> : ws_piece_unmask_kernel<1, 1, 7>;
+    const int timing = ws_k2_timing, pwin = ws_piece_win;
+    if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
     u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
-    const u32 wbit = wshift ? (u32)(pwbit < 0 ? 0 : (pwbit > 8 ? 8 : pwbit)) : 0u;
-    const u32 wn = pwn >= 2 && (P.npieces / (u64)pwn) >= 256 ? (u32)pwn : 0u;
-    const u64 ppw = wn ? (P.npieces + wn - 1) / wn
-                       : (((P.npieces + (1ull << wshift) - 1) >> wshift) + (1ull << wbit) - 1) >> wbit << wbit;
-    const u64 grid = wn ? ppw * wn : ppw << wshift;
-    const int dyn = ws_piece_lds;                                            // unused LDS: fewer blocks per CU
-    hipLaunchKernelGGL(k, dim3((u32)grid), dim3(PIECE_T), dyn > 0 && dyn <= 65536 ? dyn : 0, L.stream, L.buf, L.seg_off, L.seg_len, L.nseg,
-                       L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase, P.c_lo, P.c_hi, L.desc_base,
-                       L.desc, L.res, wshift, wbit, ppw, (u64)P.npieces, wn);
+    const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
+    const u64 grid = ppw << wshift;
+    hipLaunchKernelGGL(ws_piece_unmask_kernel<1>, dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, L.buf,
+                       L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
+                       P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni, advice);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
-    return timing ? k2_mark(L.stream, true, &tslot) : 0;
+    return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
 }
 
 // K1 + K2; K2 also holds the fallback for unordered batches. *fallback_needed: no K2
 // was launched (no pieces), so the caller must launch the gated walker itself.
-int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, int nt, unsigned char* ws, u32 gen, const u32** disorder_out,
-                    bool* fallback_needed) {
+int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,
+                    const u32** disorder_out, bool* fallback_needed) {
     PieceWs P;
-    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P);
+    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr);
     if (rc) return rc;
-    if ((rc = ws_launch_piece_unmask(L, P, nt, gen))) return rc;
+    if ((rc = ws_launch_piece_unmask(L, P, gen, advice))) return rc;
     *disorder_out = P.disorder;
     *fallback_needed = P.npieces == 0;
     return 0;

@@ -263,7 +263,6 @@ __global__ __launch_bounds__(RGAT_T) void ws_reasm_gather_kernel(const unsigned 
 // walk state and the body table (max_frames <= RSEG_TB bodies) persist across windows.
 // Each wire byte is read from HBM once (+ 1 KiB of look-ahead per extra window), each
 // body byte written once.
-extern WsOpt ws_seg_lds;
 #define RSEG_T 256
 // window = L LDS-DMA wave instructions of 1 KiB: (L-1) KiB owned + 1 KiB look-ahead;
 // L = 18 is ~20 KB of LDS: 8 workgroups (32 waves) per CU ("reasm_cfg" A/B: ws_reasm_cfg)
@@ -543,8 +542,6 @@ WsOpt ws_reasm_path{0};
 // round 1 measured it slower with the funnel-shift copy), 1 17 KiB windows at the compiler's
 // occupancy (7 waves/SIMD), 2 19 KiB windows
 WsOpt ws_reasm_cfg{0};
-WsOpt ws_reasm_merge{0}; // "reasm_merge": 1 body-boundary chunks assembled whole by one lane, 0 one
-                          // byte-store instruction from 31 lanes (default: measured faster, cfg5u 1.50 vs 1.65 ms)
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     const unsigned char* d_buf, unsigned long long buflen, const u64* d_seg_off, const u64* d_seg_len,
@@ -564,11 +561,11 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     if (fused && max_frames <= RSEG_TB) {
         auto k = rcfg == 1 ? ws_reasm_seg_kernel<18, 1> : (rcfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
         const u32 half = ws_seg_win && nseg >= 512 ? (nseg + 1) / 2 : 0;
-        const int dyn = ws_seg_lds;
-        hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), dyn > 0 && dyn <= 65536 ? dyn : 0, st, d_buf,
-                           max_frames, d_seg_off,
-                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, (u32)ws_reasm_merge,
-                           nseg, half, (u32)readcache_max_size, d_cached);
+        // (body-boundary chunks: one byte-store instruction from 31 lanes; one lane assembling
+        // them whole measured slower, cfg5u 1.65 vs 1.50 ms)
+        hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
+                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, 0u, nseg, half,
+                           (u32)readcache_max_size, d_cached);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);
     }
@@ -577,14 +574,16 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     const size_t rec_off = (piece + 255) & ~(size_t)255;
     const size_t nb_off = rec_off + nslots * sizeof(GatherRec);
     void* ws = nullptr;
-    int rc = ws_device_workspace(nb_off + (size_t)nseg * 4 + 64, st, &ws);
-    if (rc) return rc;
+    WsSlot slot;
+    int rc = slot.acquire(st);
+    if (rc || (rc = slot.workspace(nb_off + (size_t)nseg * 4 + 64, 16, &ws))) return rc;
     unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
     GatherRec* recs = reinterpret_cast<GatherRec*>(w8 + rec_off);
     u32* nbody = reinterpret_cast<u32*>(w8 + nb_off);
     WsLaunch L;
     L.buf = const_cast<unsigned char*>(d_buf); L.seg_off = d_seg_off; L.seg_len = d_seg_len; L.nseg = nseg;
-    L.max_frames = max_frames; L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
+    L.max_frames = max_frames; L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st;
+    L.cus = slot.cus; L.lds_per_cu = slot.lds;
     PieceWs P;
     if ((rc = ws_launch_piece_scan(L, 0, buflen, w8, ws_next_gen(), &P))) return rc;
     hipLaunchKernelGGL(ws_reasm_layout_kernel, dim3((u32)(((u64)nseg * RLAY_G + RLAY_T - 1) / RLAY_T)), dim3(RLAY_T), 0, st, d_buf, nseg,

@@ -156,26 +156,14 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
     if (tid == 0) ws_store_res(res + s, off, nf, status);
 }
 
-WsOpt ws_seg_lds{0};     // "seg_lds": bytes of unused dynamic LDS per segment block (occupancy A/B)
-WsOpt ws_segfuse_cfg{0}; // "segfuse_cfg": 0 256 threads, 17 KiB windows (8 workgroups/CU), 1 256 x 19 KiB,
-                          // 2 1024 x 65 KiB (one window per 64 KiB segment), 3 512 x 33 KiB
-
-int ws_launch_segfuse(const WsLaunch& L, int nt) {
+// 256 threads, 17 KiB windows (8 workgroups per CU). Measured and dropped (round 2): 19 KiB
+// windows, 1024 x 65 KiB and 512 x 33 KiB blocks, fewer blocks per CU through unused LDS
+// (5 per CU 20 % slower), plain (not nontemporal) loads and stores.
+int ws_launch_segfuse(const WsLaunch& L) {
     if (L.max_frames > SF_TB) return ws_set_msg("segfuse path: max_frames > 64");
-    void (*k)(unsigned char*, const u64*, const u64*, u32, const u64*, WebsocketFrameDesc_t*, WebsocketSegResult_t*,
-              u32, u32);
-    int T = 256;
-    switch (ws_segfuse_cfg) {
-        case 1: k = nt == 1 ? ws_segfuse_kernel<1, 20, 256> : ws_segfuse_kernel<0, 20, 256>; break;
-        case 2: k = nt == 1 ? ws_segfuse_kernel<1, 66, 1024> : ws_segfuse_kernel<0, 66, 1024>; T = 1024; break;
-        case 3: k = nt == 1 ? ws_segfuse_kernel<1, 34, 512> : ws_segfuse_kernel<0, 34, 512>; T = 512; break;
-        default: k = nt == 1 ? ws_segfuse_kernel<1, 18, 256> : ws_segfuse_kernel<0, 18, 256>;
-    }
     const u32 half = ws_seg_win && L.nseg >= 512 ? (L.nseg + 1) / 2 : 0;
-    const int dyn = ws_seg_lds;                                             // unused LDS: fewer blocks per CU
-    hipLaunchKernelGGL(k, dim3(half ? 2 * half : L.nseg), dim3(T), dyn > 0 && dyn <= 65536 ? dyn : 0, L.stream, L.buf,
-                       L.seg_off, L.seg_len,
-                       L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
+    hipLaunchKernelGGL((ws_segfuse_kernel<1, 18, 256>), dim3(half ? 2 * half : L.nseg), dim3(256), 0, L.stream, L.buf,
+                       L.seg_off, L.seg_len, L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_segfuse_kernel launch", e);
 }

@@ -1,0 +1,476 @@
+// ws_spec.hip — decode path 3, speculative form: the unmask kernel finds its own frames.
+//
+// The classic piece path (ws_piece.hip) runs K1, a walk over every frame header
+// (net_reactor.c:515-526 over websocketframe.c:112-165), and only then K2, the one-shot
+// unmask over 16 KiB pieces. K1's ~1 M scattered header lines (40 µs on cfg2) sit on the
+// critical path in front of K2. Here there is no K1:
+//
+// S1 ws_piece_spec_kernel — one 256-thread block per 16 KiB piece (K2's block shape,
+//   windows and stores). Each wave issues its payload loads, then finds the segments
+//   under its 4 KiB range (interpolation guess + 64-lane window on seg_off), reads each
+//   segment's FIRST header and predicts the frame grid so + k*g (g = that frame's wire
+//   length), parses the predicted headers that touch its range (the bytes it streams
+//   anyway, one 32-B line per frame) and XORs each frame's payload with its own key.
+//   The wave holding a predicted header verifies it (complete frame of length exactly g;
+//   after the last predicted frame an incomplete tail) and writes its descriptor; the
+//   wave holding the segment's first byte writes the predicted segment result. A
+//   mismatch flags the segment (one atomicOr per segment, the first flagger appends it to
+//   a list). The first `nchk` waves of the grid also check the segment table (ascending,
+//   inside [lo, hi)) and count themselves done on an agent-scope counter; every wave
+//   polls that counter (relaxed, bounded spin) before its stores: an unordered batch
+//   stores nothing, and a wave that gives up waiting stores nothing, tags its range and
+//   flags its segments (results never depend on dispatch order, only speed does).
+// S2 ws_piece_spec_fix_kernel — tiny unless something was flagged: unordered batch ->
+//   every segment walked exactly (ws_walk.h); flagged segments -> the speculative XOR
+//   undone (XOR is an involution; the same rule over the same header bytes) on the ranges
+//   that stored, then walked exactly.
+//
+// Why the speculation is race-free: for predicted frame k at pos = so + k*g the XOR
+// rule is "frame parses (avail = sl - k*g), MASK set, hdr < g: XOR [pos + hdr, pos + g)
+// with its key". Every input of that rule (bytes 1 and the ext length / key bytes, all in
+// [pos, pos + hdr)) lies outside every XOR range, so all waves (and S2's undo) read the
+// same original bytes whatever has been stored; for hdr >= g the rule is "no XOR"
+// whatever the other bytes hold. A verified frame has hdr + plen == g, so the rule then
+// is exactly the reference's unmask (websocketframe.c:153-158).
+//
+// State (per workspace slot, parity-double-buffered head, see ws_api.hip): head words
+// {ctr, nmis, tmo} rest at zero; S2 of call i zeroes the head of call i + 1; S2 clears
+// the flags it consumed. Not used inside HIP graph captures (the host picks the path).
+#include "ws_walk.h"
+
+#define SPEC_T 256
+#define SPEC_U WS_PIECE_U
+#define SPEC_SHIFT WS_PIECE_SHIFT
+#define SPEC_RANGE_SHIFT 12                 // one wave's range: 64 lanes x SPEC_U x 16 B = 4 KiB
+static_assert((1 << SPEC_RANGE_SHIFT) == 64 * SPEC_U * 16, "wave range");
+// bounded wait for the checkers (s_sleep 2 + a load each): option "spec_spins" (0 = give up
+// unless the first poll finds them done: exercises the repair path in tests)
+WsOpt ws_spec_spins{2048};
+
+enum { SPEC_CTR = 0, SPEC_NMIS = 1, SPEC_TMO = 2, SPEC_HEAD_WORDS = 4 };
+
+__device__ __forceinline__ u32 ld_agent(u32* p) {
+    return __hip_atomic_load(gptr<u32>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// P = the number of segments whose offset is <= a, for ascending offsets (the segment
+// holding byte a, if any, is P - 1). Interpolation guess first (exact for uniform
+// segments), then 64-ary narrowing. Bounded on any input.
+__device__ __forceinline__ u32 spec_count_le(const u64* __restrict__ seg_off, u32 nseg, u64 a, u32 guess, u32 lane) {
+    u32 lo = 0, hi = nseg;                       // off[s] <= a below lo, > a from hi (ascending input)
+    {
+        u32 w0 = guess > 31 ? guess - 31 : 0;
+        if (w0 + 64 > nseg) w0 = nseg > 64 ? nseg - 64 : 0;
+        const u32 nv = nseg - w0 < 64 ? nseg - w0 : 64;
+        const u32 i = w0 + (lane < nv ? lane : nv - 1);
+        const u32 k = (u32)__popcll(__ballot(lane < nv && seg_off[i] <= a));
+        if (k > 0 && k < nv) return w0 + k;
+        if (k == 0) {
+            if (w0 == 0) return 0;
+            hi = w0;
+        } else {
+            if (w0 + nv == nseg) return nseg;
+            lo = w0 + nv;
+        }
+    }
+    while (hi - lo > 64) {
+        const u32 step = (hi - lo) / 65;         // probes lo + step .. lo + 64 step, all < hi
+        const u32 k = (u32)__popcll(__ballot(seg_off[lo + (lane + 1) * step] <= a));
+        const u32 nlo = k ? lo + k * step + 1 : lo;
+        hi = k < 64 ? lo + (k + 1) * step : hi;
+        lo = nlo;
+    }
+    const u32 i = lo + lane;
+    return lo + (u32)__popcll(__ballot(i < hi && seg_off[i < hi ? i : lo] <= a));
+}
+
+// The prediction for one segment from its first header (bytes never changed by any wave).
+struct SpecPred {
+    u64 g;           // predicted wire length of every frame (0: no frames predicted)
+    u32 n;           // frames predicted
+    int status;      // predicted WEBSOCKET_SEG_* (OK or MAX_FRAMES)
+    bool tail;       // the reference loop parses one more header (must be incomplete)
+    bool exact;      // false: the first frame is not a plain complete frame (walked exactly by S2)
+};
+
+__device__ __forceinline__ SpecPred spec_predict(const WsHdr& h0, u64 sl, u32 max_frames) {
+    SpecPred p;
+    p.g = 0; p.n = 0; p.status = WEBSOCKET_SEG_OK; p.tail = false; p.exact = true;
+    if (sl < 2 || h0.kind == WS_PARSE_INCOMPLETE) return p;      // websocketframe.c:121-150: consumed 0
+    if (h0.kind == WS_PARSE_FRAME && h0.ret > 0 && (u64)h0.hdr + h0.plen == (u64)(u32)h0.ret) {
+        p.g = (u32)h0.ret;
+        const u64 q = sl / p.g;
+        p.n = q < max_frames ? (u32)q : max_frames;
+        const u64 used = (u64)p.n * p.g;
+        if (p.n == max_frames) p.status = used < sl ? WEBSOCKET_SEG_MAX_FRAMES : WEBSOCKET_SEG_OK;
+        else p.tail = sl - used >= 2;
+        return p;
+    }
+    p.exact = false;                                             // wrap fence, ret <= 0, (int) truncation
+    return p;
+}
+
+// header of the frame at byte p (vector loads: WEBSOCKET_BATCH_PAD makes the 32 B readable)
+__device__ __forceinline__ WsHdr spec_header(const unsigned char* p, u64 avail) {
+    const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+    const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+    const u32x4 x0 = q[0], x1 = q[1];
+    u64 h0, h1;
+    ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
+    return ws_parse(h0, h1, avail);
+}
+
+__device__ __forceinline__ void spec_flag(u32* flags, u32* list, u32* head, u32 s) {
+    const u32 old = __hip_atomic_fetch_or(gptr<u32>(flags + s), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!old) {
+        const u32 i = __hip_atomic_fetch_add(gptr<u32>(head + SPEC_NMIS), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *gptr<u32>(list + i) = s;
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
+    unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
+    u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
+    WebsocketSegResult_t* __restrict__ res, u32* head, u32* flags, u32* list, u32* marks, u32 tag, u64 pbase,
+    u64 c_lo, u64 c_hi, u64 lo, u64 hi, u64 ppw, u64 npieces, u32 wshift, u32 nchk, u32 chk_per, u32 spins) {
+    const u32 tid = threadIdx.x, lane = tid & 63;
+    const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const u32 bx = blockIdx.x;
+    // block -> piece: two windows half a batch apart (as K2, ws_piece.hip)
+    const u64 pw = (u64)(bx & ((1u << wshift) - 1u)) * ppw + (bx >> wshift);
+    const bool pvalid = pw < npieces;
+    const u64 pidx = pvalid ? pw : npieces - 1;
+    const u64 wc0 = ((pbase + pidx) << (SPEC_SHIFT - 4)) + (u64)wv * (64 * SPEC_U);
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
+    // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
+    u32x4 v[SPEC_U];
+#pragma unroll
+    for (int u = 0; u < SPEC_U; ++u) {
+        const u64 c = wc0 + (u64)(u * 64 + lane);
+        v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
+    }
+    // ---- 2. checker duty (the first nchk waves): the segment table is ascending and inside
+    //         [lo, hi) (the piece decomposition assumes it); zero-length results written here
+    const u32 gw = bx * (SPEC_T / 64) + wv;
+    if (gw < nchk) {
+        const u64 s_beg = (u64)gw * chk_per;
+        const u64 s_end = s_beg + chk_per < nseg ? s_beg + chk_per : nseg;
+        bool bad = false;
+        for (u64 sb = s_beg; sb < s_end; sb += 64) {
+            const u64 s = sb + lane;
+            if (s < s_end) {
+                const u64 so = seg_off[s], sl = seg_len[s];
+                const u64 pe = s ? seg_off[s - 1] + seg_len[s - 1] : 0;
+                bad |= pe > so || so < lo || so > hi || sl > hi - so;
+                if (sl == 0) ws_store_res(res + s, 0, 0, WEBSOCKET_SEG_OK);
+            }
+        }
+        const bool any = __ballot(bad) != 0;
+        if (lane == 0)
+            __hip_atomic_fetch_add(gptr<u32>(head + SPEC_CTR), 1u + (any ? 0x10000u : 0u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    constexpr long long RW = 64 * SPEC_U * 16;                              // this wave's bytes
+    const u64 r0 = wc0 << 4, r1 = r0 + RW;                                  // origin-relative
+    const u64 ra = r0 > lead0 ? r0 - lead0 : 0, rb = r1 - lead0;            // buffer-relative
+    const int xl = (int)lane * 16;
+    u32 cov[SPEC_U], segcov[SPEC_U];
+#pragma unroll
+    for (int u = 0; u < SPEC_U; ++u) { cov[u] = 0; segcov[u] = 0; }
+    u32 s_first = 0, s_stop = 0;                                            // segments visited [s_first, s_stop)
+    bool gave_up = false;
+    if (pvalid) {
+        // ---- 3. the segments under [ra, rb): the last one starting at or before ra, then on
+        const u64 first = seg_off[0], last_end = seg_off[nseg - 1] + seg_len[nseg - 1];
+        u32 guess = 0;
+        if (ra > first && last_end > first) {
+            const double f = (double)(ra - first) / (double)(last_end - first);
+            guess = f >= 1.0 ? nseg - 1 : (u32)(f * (double)nseg);
+            if (guess >= nseg) guess = nseg - 1;
+        }
+        const u32 P = spec_count_le(seg_off, nseg, ra, guess, lane);
+        u32 s = P ? P - 1 : 0;
+        s_first = s;
+        for (u32 it = 1; s < nseg; ++s, ++it) {
+            if ((it & 63) == 0) {                                           // an unordered batch stores nothing:
+                u32 c = lane == 0 ? ld_agent(head + SPEC_CTR) : 0u;         // stop walking garbage early
+                if (__builtin_amdgcn_readfirstlane(c) >> 16) break;
+            }
+            const u64 so = seg_off[s], sl = seg_len[s];
+            if (so >= rb) break;
+            if (sl == 0 || (so < ra && sl <= ra - so)) continue;           // empty, or ends before the range
+            const u64 sorg = so + lead0;
+            {   // byte coverage by segments: chunks wholly inside segments are stored whole
+                const long long sa = (long long)(sorg - r0), sbb = sa + (long long)sl;
+                const int SA = (int)(sa < -16 ? -16 : (sa > RW + 16 ? RW + 16 : sa));
+                const int SB = (int)(sbb < -16 ? -16 : (sbb > RW + 16 ? RW + 16 : sbb));
+#pragma unroll
+                for (int u = 0; u < SPEC_U; ++u) {
+                    const int x = u * 1024 + xl;
+                    const int l2 = SA > x ? (SA - x < 16 ? SA - x : 16) : 0;
+                    const int h2 = SB > x ? (SB - x < 16 ? SB - x : 16) : 0;
+                    if (h2 > l2) segcov[u] |= (0xFFFFu >> (16 - h2)) & (0xFFFFu << l2);
+                }
+            }
+            // first header (an unordered batch may name any offset: keep the loads in the buffer)
+            const u64 soc = so <= hi ? so : hi;
+            const WsHdr h0 = spec_header(buf + soc, sl);
+            const SpecPred pr = spec_predict(h0, sl, max_frames);
+            bool bad = !pr.exact;
+            if (lane == 0 && sorg >= r0 && sorg < r1)                       // result: the wave holding byte 0
+                ws_store_res(res + s, (u64)pr.n * pr.g, pr.n, pr.status);
+            const u64 kend = (u64)pr.n + (pr.tail ? 1u : 0u);               // + the tail header to check
+            if (kend) {
+                const u64 g = pr.g;
+                const u64 kA = r0 > sorg ? (r0 - sorg) / g : 0;              // frame holding r0
+                u64 kB = (r1 - sorg + g - 1) / g;                           // frames starting before r1
+                if (kB > kend) kB = kend;
+                const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
+                for (u64 kk = kA; kk < kB; kk += 64) {
+                    const u64 k = kk + lane;
+                    const bool act = k < kB;
+                    const u64 kc = act ? k : kA;
+                    const u64 pos = so + kc * g;
+                    const WsHdr h = spec_header(buf + pos, sl - kc * g);
+                    const u64 porg = pos + lead0;
+                    const bool tail = act && pr.tail && k == pr.n;
+                    bool b = false;
+                    if (act && porg >= r0 && porg < r1) {                   // this wave owns the header
+                        if (tail) b = h.kind != WS_PARSE_INCOMPLETE;
+                        else if (h.kind == WS_PARSE_FRAME && (u64)h.hdr + h.plen == g) ws_store_desc(desc + dbase + k, pos, h);
+                        else b = true;
+                    }
+                    if (__ballot(b)) bad = true;
+                    // the XOR rule (see the top of the file)
+                    const bool x = act && !tail && h.kind == WS_PARSE_FRAME && h.masked && h.hdr < g;
+                    const u64 p0 = porg + h.hdr, p1 = porg + g;
+                    const long long qa = (long long)(p0 - r0), qb = (long long)(p1 - r0);
+                    const int A = (int)(qa < -16 ? -16 : (qa > RW + 16 ? RW + 16 : qa));
+                    const int B = (int)(qb < -16 ? -16 : (qb > RW + 16 ? RW + 16 : qb));
+                    const u32 rk = rotl32(h.key, 8u * (u32)(p0 & 3));
+                    u64 hm = __ballot(x && p1 > r0 && p0 < r1);
+                    while (hm) {
+                        const int i = __builtin_ctzll(hm);
+                        hm &= hm - 1;
+                        const int a = __builtin_amdgcn_readlane(A, i), bb = __builtin_amdgcn_readlane(B, i);
+                        const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
+#pragma unroll
+                        for (int u = 0; u < SPEC_U; ++u) {
+                            if (bb <= u * 1024 || a >= u * 1024 + 1024) continue;   // (uniform) not in row u
+                            const int xx = u * 1024 + xl;
+                            const int l2 = a > xx ? a - xx : 0, h2 = bb < xx + 16 ? bb - xx : 16;
+                            if (h2 <= l2) continue;
+                            ws_xor_range(key, l2, h2, v[u], cov[u]);
+                        }
+                    }
+                }
+            }
+            if (bad && lane == 0) spec_flag(flags, list, head, s);
+        }
+        s_stop = s < nseg ? s + 1 : nseg;
+    }
+    // ---- 4. wait for the checkers (bounded), then store
+    u32 c = 0;
+    if (lane == 0) {
+        c = ld_agent(head + SPEC_CTR);
+        for (u32 n = 0; (c & 0xFFFFu) < nchk && n < spins; ++n) {
+            __builtin_amdgcn_s_sleep(2);
+            c = ld_agent(head + SPEC_CTR);
+        }
+    }
+    c = (u32)__builtin_amdgcn_readlane((int)c, 0);
+    const bool unordered = (c >> 16) != 0;
+    if (!pvalid || unordered) return;                                       // S2 walks an unordered batch
+    if ((c & 0xFFFFu) < nchk) {
+        // gave up waiting: store nothing; S2 finishes this range's segments (their XOR is
+        // undone on the ranges that did store, then they are walked exactly)
+        gave_up = true;
+        if (lane == 0) {
+            *gptr<u32>(marks + ((r0 >> SPEC_RANGE_SHIFT) - (pbase << (SPEC_SHIFT - SPEC_RANGE_SHIFT)))) = tag;
+            __hip_atomic_fetch_add(gptr<u32>(head + SPEC_TMO), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (u32 s = s_first; s < s_stop; ++s) {
+                const u64 so = seg_off[s], sl = seg_len[s];
+                if (sl && !(so < ra && sl <= ra - so) && so < rb) spec_flag(flags, list, head, s);
+            }
+        }
+        return;
+    }
+    (void)gave_up;
+#pragma unroll
+    for (int u = 0; u < SPEC_U; ++u) {
+        const u64 cidx = wc0 + (u64)(u * 64 + lane);
+        if (!cov[u] || cidx < c_lo || cidx >= c_hi) continue;
+        const u32x4 w = v[u];
+        if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) st16<NT>(w, base + cidx);
+        else ws_store_bytes(reinterpret_cast<gu8*>(base + cidx), w, cov[u]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// S2: repair. One wave per segment, vector loads only (the wave rewrites payload bytes and
+// then reads headers that may lie in them; the scalar cache would keep stale lines).
+
+// unmask [P0, P1) by one wave, skipping the 4 KiB wave ranges whose S1 wave stored nothing
+template <int NT>
+__device__ __forceinline__ void spec_xor_stored(unsigned char* buf, unsigned char* P0, unsigned char* P1, u32 key,
+                                                const u32* marks, u32 tag, u64 rbase, bool any_tmo, u32 lane) {
+    if (!any_tmo) {
+        unmask_payload<4, NT>(P0, P1, key, lane);
+        return;
+    }
+    const uintptr_t org = reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15;
+    uintptr_t a = reinterpret_cast<uintptr_t>(P0);
+    const uintptr_t e = reinterpret_cast<uintptr_t>(P1);
+    while (a < e) {
+        const u64 r = (u64)(a - org) >> SPEC_RANGE_SHIFT;
+        uintptr_t b = org + ((uintptr_t)(r + 1) << SPEC_RANGE_SHIFT);
+        if (b > e) b = e;
+        if (marks[r - rbase] != tag) {
+            // the key phase follows the byte's distance from P0
+            const u32 sh = 8u * (u32)((a - reinterpret_cast<uintptr_t>(P0)) & 3);
+            unmask_payload<4, NT>(reinterpret_cast<unsigned char*>(a), reinterpret_cast<unsigned char*>(b),
+                                  sh ? (key >> sh) | (key << (32 - sh)) : key, lane);
+        }
+        a = b;
+    }
+}
+
+// the reactor loop over segment s with vector header loads (ws_walk.h:walk_segment otherwise)
+template <int NT>
+__device__ __forceinline__ void spec_walk(unsigned char* __restrict__ buf, u32 s, const u64* __restrict__ seg_off,
+                                          const u64* __restrict__ seg_len, u32 max_frames,
+                                          const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
+                                          WebsocketSegResult_t* __restrict__ res, u32 lane) {
+    const u64 so = seg_off[s], sl = seg_len[s];
+    const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
+    unsigned char* const seg = buf + so;
+    u64 off = 0;
+    u32 nf = 0;
+    int status = WEBSOCKET_SEG_OK;
+    while (off < sl) {
+        if (nf >= max_frames) { status = WEBSOCKET_SEG_MAX_FRAMES; break; }
+        if (sl - off < 2) break;                                        // websocketframe.c:121
+        unsigned char* const p = seg + off;
+        const WsHdr h = spec_header(p, sl - off);
+        if (h.kind == WS_PARSE_INCOMPLETE) break;
+        if (h.kind == WS_PARSE_WRAP) { status = WEBSOCKET_SEG_ERR_LEN_WRAP; break; }
+        if (h.masked) unmask_payload<4, NT>(p + h.hdr, p + h.hdr + h.plen, h.key, lane);
+        if (h.ret == 0) break;                                          // (int) truncated to 0
+        if (lane == 0) ws_store_desc(desc + dbase + nf, so + off, h);
+        ++nf;
+        if (h.ret < 0) { status = WEBSOCKET_SEG_ERR_DECODE; break; }    // net_reactor.c:518-520
+        off += (u32)h.ret;                                              // net_reactor.c:525
+    }
+    if (lane == 0) ws_store_res(res + s, off, nf, status);
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void ws_piece_spec_fix_kernel(
+    unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
+    u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
+    WebsocketSegResult_t* __restrict__ res, const u32* head, u32* next_head, u32* flags, const u32* list,
+    const u32* marks, u32 tag, u64 pbase, int* advice) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u32 nw = gridDim.x * 4;
+    const u32 c = *gptr<u32>(head + SPEC_CTR), nmis = *gptr<u32>(head + SPEC_NMIS);
+    const bool tmo = *gptr<u32>(head + SPEC_TMO) != 0;
+    const u64 rbase = pbase << (SPEC_SHIFT - SPEC_RANGE_SHIFT);
+    if (c >> 16) {
+        // unordered (or outside [lo, hi)): S1 stored nothing; the reactor loop per segment
+        for (u32 s = gw; s < nseg; s += nw) spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
+        for (u32 i = gw * 64 + lane; i < nmis; i += nw * 64) *gptr<u32>(flags + list[i]) = 0;
+    } else {
+        for (u32 i = gw; i < nmis; i += nw) {
+            const u32 s = list[i];
+            const u64 so = seg_off[s], sl = seg_len[s];
+            const WsHdr h0 = spec_header(buf + so, sl);
+            const SpecPred pr = spec_predict(h0, sl, max_frames);
+            for (u32 k = 0; k < pr.n; ++k) {                           // undo S1's XOR where it stored
+                unsigned char* const p = buf + so + (u64)k * pr.g;
+                const WsHdr h = spec_header(p, sl - (u64)k * pr.g);
+                if (h.kind == WS_PARSE_FRAME && h.masked && h.hdr < pr.g)
+                    spec_xor_stored<NT>(buf, p + h.hdr, p + pr.g, h.key, marks, tag, rbase, tmo, lane);
+            }
+            spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
+            if (lane == 0) *gptr<u32>(flags + s) = 0;
+        }
+    }
+    if (gw == 0 && lane == 0) {
+        // the next call's head rests at zero; advice for the host's next path choice: stay
+        // speculative while at most 1/32 of the segments needed the exact walk
+        gu32* nh = gptr<u32>(next_head);
+        nh[SPEC_CTR] = 0;
+        nh[SPEC_NMIS] = 0;
+        nh[SPEC_TMO] = 0;
+        if (advice)
+            __hip_atomic_store(advice, (c >> 16) == 0 && (u64)nmis * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+extern WsOpt ws_piece_win;
+extern WsOpt ws_piece_lds;
+extern WsOpt ws_k2_timing;
+int ws_k2_mark(hipStream_t st, bool end, size_t* slot);
+
+// spec workspace: [head A: 4 u32][head B: 4 u32][pad to 64][flags: nseg u32][list: nseg u32][marks: ranges u32]
+size_t ws_spec_workspace_bytes(u64 span, u32 nseg) {
+    const u64 ranges = ((span + 15) >> SPEC_RANGE_SHIFT) + 8;
+    return 64 + (size_t)nseg * 8 + (size_t)ranges * 4 + 64;
+}
+
+// bytes that must be zero when the workspace is (re)allocated: heads + flags
+size_t ws_spec_zero_bytes(u32 nseg) { return 64 + (size_t)nseg * 4; }
+
+// S1 can run only when its checkers are a small part of the grid: <= 1024 waves of <= 256 segments
+bool ws_spec_fits(u64 span, u32 nseg) {
+    const u64 npieces = (span + (1ull << SPEC_SHIFT) - 1) >> SPEC_SHIFT;
+    const u64 waves = (npieces + 2) * (SPEC_T / 64);
+    const u64 nchk = waves < 1024 ? waves : 1024;
+    return npieces >= 1 && nseg >= 1 && (u64)nseg <= nchk * 256;
+}
+
+int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, int* advice_dev) {
+    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
+    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
+    const u64 npieces = hi_org > lo_org ? ((hi_org - 1) >> SPEC_SHIFT) - (lo_org >> SPEC_SHIFT) + 1 : 0;
+    if (!npieces) return ws_set_msg("spec decode: empty range");
+    const u64 pbase = lo_org >> SPEC_SHIFT, c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
+    u32* head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * (parity & 1);
+    u32* next_head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * ((parity + 1) & 1);
+    u32* flags = reinterpret_cast<u32*>(sws + 64);
+    u32* list = flags + L.nseg;
+    u32* marks = list + L.nseg;
+    const int pwin = ws_piece_win;
+    u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
+    while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
+    const u64 ppw = (npieces + (1ull << wshift) - 1) >> wshift;
+    const u64 grid = ppw << wshift;
+    const u64 waves = grid * (SPEC_T / 64);
+    const u32 nchk = (u32)(waves < 1024 ? waves : 1024);
+    const u32 chk_per = (u32)((L.nseg + nchk - 1) / nchk);
+    if (chk_per > 256) return ws_set_msg("spec decode: too many segments for the checkers");
+    size_t tslot = 0;
+    int rc;
+    const int timing = ws_k2_timing;
+    if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
+    const int dyn = ws_piece_lds;
+    hipLaunchKernelGGL(ws_piece_spec_kernel<1>, dim3((u32)grid), dim3(SPEC_T), dyn > 0 && dyn <= 65536 ? dyn : 0,
+                       L.stream, L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head,
+                       flags, list, marks, tag, pbase, c_lo, c_hi, lo, hi, ppw, npieces, wshift, nchk, chk_per,
+                       (u32)(int)ws_spec_spins);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ws_set_err("ws_piece_spec_kernel launch", e);
+    if (timing && (rc = ws_k2_mark(L.stream, true, &tslot))) return rc;
+    const u32 fix_blocks = (u32)((L.nseg + 3) / 4 < 256 ? (L.nseg + 3) / 4 : 256);
+    hipLaunchKernelGGL(ws_piece_spec_fix_kernel<1>, dim3(fix_blocks), dim3(256), 0, L.stream, L.buf, L.seg_off,
+                       L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, next_head, flags, list,
+                       marks, tag, pbase, advice_dev);
+    e = hipGetLastError();
+    if (e != hipSuccess) return ws_set_err("ws_piece_spec_fix_kernel launch", e);
+    return 0;
+}

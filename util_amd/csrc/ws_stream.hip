@@ -896,15 +896,13 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     if (lane == 0) plan->nrows = rows;
 }
 
-int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, int nt, u32 gen);
-
 WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
 
-// scratch for the chunk-parallel walk: the calling stream's auxiliary workspace (device
+// scratch for the chunk-parallel walk: the call's slot's auxiliary workspace (device
 // records + counters, and a pinned host copy of them), so concurrent calls on different
 // streams never share it (the walk runs in eager calls only)
 struct RwScratch {
@@ -913,9 +911,9 @@ struct RwScratch {
 };
 
 // (the aux head holds the pass loop's state: the walk's scratch starts after it)
-static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch* out) {
+static int rw_scratch(WsSlot& slot, size_t dbytes, size_t hbytes, RwScratch* out) {
     WsAux A;
-    const int rc = ws_aux_workspace(WS_AUX_HEAD + dbytes, WS_AUX_HEAD + hbytes, st, &A);
+    const int rc = slot.aux(WS_AUX_HEAD + dbytes, WS_AUX_HEAD + hbytes, &A);
     if (rc) return rc;
     out->d = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
     out->h = reinterpret_cast<unsigned char*>(A.h) + WS_AUX_HEAD;
@@ -926,8 +924,8 @@ static int rw_scratch(size_t dbytes, size_t hbytes, hipStream_t st, RwScratch* o
 // The chunk-parallel walk of [P, len) with nf frames before P (see above). Launches the
 // emit kernels and, for chunks without a link, one-wavefront chunk walks; the last of
 // them writes the tail pointers, item count and segment result.
-static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames, WebsocketFrameDesc_t* d_desc,
-                   const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st) {
+static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
+                   WebsocketFrameDesc_t* d_desc, const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st) {
     hipError_t e;
     int rc;
     ws_stat_rw_chunk_walks = 0;
@@ -950,7 +948,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         return ho[2] ? 1 : 0;
     };
     // sample: the first RW_SAMPLE bytes, and the mean wire length
-    if ((rc = rw_scratch(256, 256, st, &S))) return rc;
+    if ((rc = rw_scratch(slot, 256, 256, &S))) return rc;
     wout = reinterpret_cast<u64*>(S.d);
     ho = reinterpret_cast<u64*>(S.h);
     u64 P1 = 0;
@@ -966,7 +964,8 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_walk_kernel launch", e);
         return 0;
     }
-    const u64 cmax = ws_stream_rw_cmax >= 16 && ws_stream_rw_cmax <= 26 ? 1ull << ws_stream_rw_cmax : RW_CMAX;
+    const int cmax_log = ws_stream_rw_cmax;                                  // one read per call
+    const u64 cmax = cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX;
     const u64 C = rw_pow2_clamp(mean * 1024, RW_CMIN, cmax);
     const u32 H = (u32)rw_pow2_clamp(mean * 8, RW_HMIN, C / 2 < RW_HMAX ? C / 2 : RW_HMAX);
     const u64 nchunks = (len - P + C - 1) / C;
@@ -981,7 +980,7 @@ static int rw_walk(unsigned char* d_buf, u64 len, u64 P, u32 nf, u32 max_frames,
     const u32 capc = H / 32;                                                 // candidates: 1/32 of a window
     const size_t b_cand = (size_t)nchunks * capc * 8;
     const size_t b_host = b_recs + b_nrec + b_dx + 256 + b_own;              // copied back
-    if ((rc = rw_scratch(256 + b_host + b_tab + b_stg + b_cand, 256 + b_host, st, &S))) return rc;
+    if ((rc = rw_scratch(slot, 256 + b_host + b_tab + b_stg + b_cand, 256 + b_host, &S))) return rc;
     unsigned char* w = reinterpret_cast<unsigned char*>(S.d);
     unsigned char* hw = reinterpret_cast<unsigned char*>(S.h);
     wout = reinterpret_cast<u64*>(w);
@@ -1130,7 +1129,8 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     u64* tab = reinterpret_cast<u64*>(w + L.o_tab);
     u32* stg = reinterpret_cast<u32*>(w + L.o_stg);
     u64* cand = reinterpret_cast<u64*>(w + L.o_cand);
-    const u64 cmax = ws_stream_rw_cmax >= 16 && ws_stream_rw_cmax <= 26 ? 1ull << ws_stream_rw_cmax : RW_CMAX;
+    const int cmax_log = ws_stream_rw_cmax;                                  // one read per call
+    const u64 cmax = cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX;
     hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
@@ -1166,8 +1166,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     // of the stream's auxiliary workspace
     const size_t pws = ws_piece_workspace_bytes(len, 1, max_frames);
     void* ws = nullptr;
-    int rc = ws_device_workspace(pws + 64, st, &ws);
-    if (rc) return rc;
+    WsSlot slot;                              // every buffer of this call comes from one pinned slot
+    int rc = slot.acquire(st);
+    if (rc || (rc = slot.workspace(pws + 64, 16, &ws))) return rc;
     unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
     u64* d_seg = reinterpret_cast<u64*>(w8 + ((pws + 15) & ~(size_t)15));    // [0] offset 0, [1] length
     const bool capture = ws_capturing(st);
@@ -1176,19 +1177,21 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     // round while rounds pay, the chunk-parallel walk once lengths keep changing. A captured
     // call (and any shorter stream) never reads it: `nr` rounds, the last one's resolve also
     // walks whatever is left with one wavefront.
-    const bool host_rw = ws_stream_rw && len >= RW_MIN && !capture;
+    const bool rw = ws_stream_rw != 0;
+    const bool host_rw = rw && len >= RW_MIN && !capture;
     // a captured call on a long stream runs the chunk-parallel walk on the device (its
     // scratch, sized from the length, follows the state in the aux workspace)
-    const bool dev_rw = ws_stream_rw && len >= RW_MIN && capture;
+    const bool dev_rw = rw && len >= RW_MIN && capture;
     const RwDevLayout RL = dev_rw ? rw_dev_layout(len) : RwDevLayout{};
     WsAux A;
-    if ((rc = ws_aux_workspace(WS_AUX_HEAD + (dev_rw ? RL.bytes : 0), host_rw ? WS_AUX_HEAD : 0, st, &A))) return rc;
+    if ((rc = slot.aux(WS_AUX_HEAD + (dev_rw ? RL.bytes : 0), host_rw ? WS_AUX_HEAD : 0, &A))) return rc;
     SdState* sd = reinterpret_cast<SdState*>(A.d);
     SdMirror* hm = host_rw ? reinterpret_cast<SdMirror*>(A.h) : nullptr;
     SdMirror* dm = host_rw ? reinterpret_cast<SdMirror*>(A.h_dev) : nullptr;
     WsLaunch L;
     L.buf = d_buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
-    L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st; L.cus = 0;
+    L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st;
+    L.cus = slot.cus; L.lds_per_cu = slot.lds;
     PieceWs Pw;
     const u32 gen = ws_next_gen();
     // the piece-path views of the workspace
@@ -1199,6 +1202,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         Pw.c_lo = 0;
         Pw.c_hi = (len + lead0 + 15) >> 4;
         Pw.disorder = reinterpret_cast<u32*>(w8);
+        Pw.nonuni = reinterpret_cast<u32*>(w8) + 1;
         Pw.ptr = reinterpret_cast<u64*>(w8 + 16);
         size_t b = (16 + Pw.npieces * 8 + 15) & ~(size_t)15;
         Pw.nwork = reinterpret_cast<u32*>(w8 + b);
@@ -1227,19 +1231,19 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         const hipError_t e2 = hipGetLastError();
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
-    const int nr = ws_stream_rounds >= 1 && ws_stream_rounds <= 64 ? (int)ws_stream_rounds : 4;
+    const int nr0 = ws_stream_rounds, nr = nr0 >= 1 && nr0 <= 64 ? nr0 : 4;
     if (dev_rw) {
         if ((rc = rounds(nr, false, 0))) return rc;
         if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
                                  reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL)))
             return rc;
         *A.state_ok = true;
-        return ws_launch_piece_unmask(L, Pw, 1, gen);
+        return ws_launch_piece_unmask(L, Pw, gen);
     }
     if (!host_rw) {
         if ((rc = rounds(nr, true, 0))) return rc;
         *A.state_ok = true;
-        return ws_launch_piece_unmask(L, Pw, 1, gen);
+        return ws_launch_piece_unmask(L, Pw, gen);
     }
     // eager: one round, then follow the published state
     auto published = [&](u32 tag) -> int {
@@ -1267,12 +1271,12 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         const u64 P = hm->P;
         const u32 nf = hm->nf;
         if (len - P >= RW_MIN) {                                             // lengths keep changing
-            if ((rc = rw_walk(d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
+            if ((rc = rw_walk(slot, d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
         } else {
             hipLaunchKernelGGL(ws_stream_finish_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, max_frames, d_desc,
                                Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, sd);
             if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_stream_finish_kernel launch", e);
         }
     }
-    return ws_launch_piece_unmask(L, Pw, 1, gen);
+    return ws_launch_piece_unmask(L, Pw, gen);
 }
