@@ -81,7 +81,7 @@ __device__ __forceinline__ u32 spec_count_le(const u64* __restrict__ seg_off, u3
         lo = nlo;
     }
     const u32 i = lo + lane;
-    return lo + (u32)__popcll(__ballot(i < hi && seg_off[i < hi ? i : lo] <= a));
+    return lo + (u32)__popcll(__ballot(i < hi && seg_off[i < nseg ? i : nseg - 1] <= a));
 }
 
 // The prediction for one segment from its first header (bytes never changed by any wave).
@@ -201,6 +201,10 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
             const u64 so = seg_off[s], sl = seg_len[s];
             if (so >= rb) break;
             if (sl == 0 || (so < ra && sl <= ra - so)) continue;           // empty, or ends before the range
+            if (so > hi || sl > hi - so) {                                  // outside the batch: the checkers
+                if (lane == 0) spec_flag(flags, list, head, s);             // mark it unordered, nothing is
+                continue;                                                   // stored; never load past it
+            }
             const u64 sorg = so + lead0;
             {   // byte coverage by segments: chunks wholly inside segments are stored whole
                 const long long sa = (long long)(sorg - r0), sbb = sa + (long long)sl;
@@ -214,9 +218,7 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                     if (h2 > l2) segcov[u] |= (0xFFFFu >> (16 - h2)) & (0xFFFFu << l2);
                 }
             }
-            // first header (an unordered batch may name any offset: keep the loads in the buffer)
-            const u64 soc = so <= hi ? so : hi;
-            const WsHdr h0 = spec_header(buf + soc, sl);
+            const WsHdr h0 = spec_header(buf + so, sl);
             const SpecPred pr = spec_predict(h0, sl, max_frames);
             bool bad = !pr.exact;
             if (lane == 0 && sorg >= r0 && sorg < r1)                       // result: the wave holding byte 0
