@@ -802,6 +802,37 @@ def run_inflight(args, wl0, dev, world, rank):
                     "not part of value", "verified": mism == 0}, mism
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks of this same command as
+    child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, one GPU
+    each; WS_BENCH_RANKS_PER_GPU > 1 packs ranks onto fewer GPUs for rehearsal), relay rank 0's
+    JSON line, and return non-zero if any rank failed. This process never touches a GPU."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [p.wait() for p in procs]
+    if out:
+        _RESULT_OUT.write(out.decode())
+        _RESULT_OUT.flush()
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc]
+    if bad:
+        sys.stderr.write("bench.py: ranks failed: %s\n" % bad)
+    return 1 if bad or not out else 0
+
+
 def main():
     # the contract's single JSON line goes to the real stdout; everything else any library
     # prints to fd 1 (gloo's "Rank k is connected to ..." lines, runtime chatter) to stderr
@@ -841,6 +872,19 @@ def main():
                          "decode + message reassembly (use with --config cfg5), or the whole batch as ONE raw "
                          "rx stream with no frame offsets (device-side boundary discovery)")
     args = ap.parse_args()
+    # --gpus N means N ranks: launched here (one child process per GPU, before anything touches
+    # a GPU) unless a launcher (torchrun) already set WORLD_SIZE, which must then equal N
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif os.environ.get("WS_BENCH_LAUNCH_ECHO"):                   # launcher test (tests/test_dist.py)
+        emit({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
+              "local_rank": int(os.environ["LOCAL_RANK"]), "master_port": os.environ["MASTER_PORT"]})
+        sys.exit(int(os.environ.get("WS_BENCH_LAUNCH_ECHO_RC", "0")) if os.environ["RANK"] != "0" else 0)
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%s: refusing to report a %s-rank run as %d GPUs\n"
+                         % (args.gpus, os.environ["WORLD_SIZE"], os.environ["WORLD_SIZE"], args.gpus))
+        sys.exit(2)
     from util_amd import wsframe as W
     path = DEFAULT_PATH if args.path is None else args.path
     if args.path is not None:

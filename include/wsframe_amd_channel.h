@@ -73,11 +73,14 @@ typedef struct WebsocketBatchCursor_t {
 
 /* on_decode from a batch: the next descriptor of `cursor`, which must describe the frame at
  * buf (buf == inbuf + frame_off - seg_off; else err = 1: the loop left the batch's walk).
- * Past the last descriptor: ERR_DECODE ended the walk with that descriptor (its ret < 0 gave
- * err already); otherwise the bytes from here on were not decoded by the batch (incomplete
- * tail, or MAX_FRAMES) -> incomplete = 1, so the reactor keeps them for the next batch
- * (net_reactor.c:536-539). Cursor-based: call it from an on_decode that finds the cursor
- * (e.g. through NetChannel_t.userdata). */
+ * Past the last descriptor, by the segment's stop reason: OK -> incomplete = 1 (an
+ * incomplete tail: the reactor keeps it, net_reactor.c:536-539, and it leads the next
+ * read's segment, which starts at m_inbuf[0]); MAX_FRAMES -> the frame at buf is decoded on
+ * the host (websocketframeOnDecode), so a short descriptor capacity never stalls a
+ * connection; ERR_LEN_WRAP / ERR_DECODE -> err = 1 (the channel is closed, :518-520).
+ * Cursor-based: call it from an on_decode that finds the cursor (e.g. through
+ * NetChannel_t.userdata); one cursor per read (recv for every readable
+ * channel, one batch over their whole m_inbuf, then each channel's on_read loop). */
 WSFRAME_AMD_EXPORT void websocketframeOnDecodeBatch(WebsocketBatchCursor_t* cursor, unsigned char* buf, size_t len,
                                                     struct NetChannelInbufDecodeResult_t* result);
 

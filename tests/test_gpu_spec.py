@@ -33,6 +33,7 @@ def forced_spec():
     W.set_option("path", -1)
     W.set_option("piece_spec", 1)
     W.set_option("spec_spins", 2048)
+    W.set_option("spec_g", 0)
 
 
 def frame(rng, plen, masked=True, form=None, b0=0x82):
@@ -68,7 +69,13 @@ def spec_calls():
     return W.get_stat("piece_spec_calls")
 
 
-def check(dev, wire, so, sl, max_frames, tag, expect_spec=True, desc_base=None):
+def wirelen(plen, masked=True):
+    return plen + (2 if plen < 126 else (4 if plen <= 0xFFFF else 10)) + (4 if masked else 0)
+
+
+def check(dev, wire, so, sl, max_frames, tag, g, expect_spec=True, desc_base=None):
+    """decode speculatively predicting frames of wire length g (the host's hint), vs the oracle"""
+    W.set_option("spec_g", g)
     n0 = spec_calls()
     out = P.assert_same(dev, wire, so, sl, max_frames, desc_base=desc_base, tag=tag)
     if expect_spec:
@@ -111,8 +118,8 @@ def test_misprediction_at_every_frame_index(dev, kind, plen):
             parts[1 + j % 15] = anomalous(rng, kind, plen)
         segs.append(parts)
     wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, 16, "%s plen %d" % (kind, plen))
-    check(dev, wire, so, sl, 20, "%s plen %d max 20" % (kind, plen))
+    check(dev, wire, so, sl, 16, "%s plen %d" % (kind, plen), wirelen(plen))
+    check(dev, wire, so, sl, 20, "%s plen %d max 20" % (kind, plen), wirelen(plen))
 
 
 @pytest.mark.parametrize("tail", ["exact", "hdr1", "hdr5", "payload_short", "shorter_complete", "garbage",
@@ -131,7 +138,7 @@ def test_segment_tails(dev, tail):
                  "longer_incomplete": frame(rng, 5000)[:650], "zero_frame": frame(rng, 0)}[tail]
         segs.append(parts + [extra])
     wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, 17, tail)
+    check(dev, wire, so, sl, 17, tail, wirelen(700))
 
 
 @pytest.mark.parametrize("max_frames", [1, 2, 7, 16, 64])
@@ -141,7 +148,7 @@ def test_max_frames(dev, max_frames):
     rng = np.random.default_rng(max_frames)
     segs = [[frame(rng, 300) for _ in range(16)] + ([frame(rng, 300)[:100]] if j % 2 else []) for j in range(64)]
     wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, max_frames, "max_frames %d" % max_frames)
+    check(dev, wire, so, sl, max_frames, "max_frames %d" % max_frames, wirelen(300))
 
 
 def test_first_frame_quirks(dev):
@@ -154,7 +161,8 @@ def test_first_frame_quirks(dev):
     segs = [[wrap], [wrap_unmasked], [b""], [b"\x82"], [frame(rng, 50)[:6]], [frame(rng, 70) * 3],
             [frame(rng, 0) for _ in range(10)], [frame(rng, 1) for _ in range(40)]]
     wire, so, sl = batch(segs * 20, rng)
-    check(dev, wire, so, sl, 64, "quirks")
+    for g in (wirelen(20), wirelen(0), wirelen(1), 2, 10):
+        check(dev, wire, so, sl, 64, "quirks g %d" % g, g)
 
 
 def test_garbage_and_random_streams(dev):
@@ -164,9 +172,11 @@ def test_garbage_and_random_streams(dev):
     n = 1 << 20
     wire = rng.integers(0, 256, n, dtype=np.uint8)
     cuts = np.sort(rng.choice(n, 3000, replace=False))
-    check(dev, wire, [int(x) for x in cuts[:-1]], [int(b - a) for a, b in zip(cuts[:-1], cuts[1:])], 32, "garbage")
+    check(dev, wire, [int(x) for x in cuts[:-1]], [int(b - a) for a, b in zip(cuts[:-1], cuts[1:])], 32, "garbage",
+          100)
     wire, so, sl = P.random_stream(np.random.default_rng(22), 2000)
-    check(dev, wire, so, sl, 16, "random")
+    for g in (6, 131, 1006, 4104):
+        check(dev, wire, so, sl, 16, "random g %d" % g, g)
 
 
 def test_unordered_and_out_of_range(dev):
@@ -176,11 +186,12 @@ def test_unordered_and_out_of_range(dev):
     segs = [[frame(rng, 900) for _ in range(16)] for _ in range(200)]
     wire, so, sl = batch(segs, rng)
     perm = rng.permutation(len(so))
-    check(dev, wire, [so[i] for i in perm], [sl[i] for i in perm], 16, "unordered")
+    check(dev, wire, [so[i] for i in perm], [sl[i] for i in perm], 16, "unordered", wirelen(900))
     so2, sl2 = list(so), list(sl)
     so2[50], so2[51] = so2[51], so2[50]
     sl2[50], sl2[51] = sl2[51], sl2[50]
-    check(dev, wire, so2, sl2, 16, "one swap")
+    check(dev, wire, so2, sl2, 16, "one swap", wirelen(900))
+    W.set_option("spec_g", wirelen(900))
     n = len(wire)
     d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
     d[:n] = torch.from_numpy(wire).to(dev)
@@ -199,6 +210,15 @@ def test_unordered_and_out_of_range(dev):
     assert np.array_equal(d[:n].cpu().numpy(), ob)
 
 
+def test_wrong_frame_length_hint(dev):
+    """a hint that matches no segment (the previous call's frames were another size): every
+    segment mispredicts at its first frame and is repaired"""
+    rng = np.random.default_rng(70)
+    wire, so, sl = batch([[frame(rng, 1000) for _ in range(16)] for _ in range(200)], rng)
+    for g in (wirelen(4096), wirelen(999), wirelen(1001), 2, wirelen(1000) * 2):
+        check(dev, wire, so, sl, 16, "hint %d" % g, g)
+
+
 @pytest.mark.parametrize("spins", [0, 1])
 def test_checker_give_up_path(dev, spins):
     """waves that stop waiting for the table checkers store nothing and tag their 4 KiB range;
@@ -210,9 +230,9 @@ def test_checker_give_up_path(dev, spins):
     for j in range(0, 300, 7):
         segs[j][3 + j % 12] = frame(rng, 4000)
     wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, 16, "spins %d" % spins)
+    check(dev, wire, so, sl, 16, "spins %d" % spins, wirelen(4096))
     wire, so, sl = P.random_stream(np.random.default_rng(31), 1500)
-    check(dev, wire, so, sl, 16, "spins %d random" % spins)
+    check(dev, wire, so, sl, 16, "spins %d random" % spins, 1006)
 
 
 def test_desc_base_and_empty_segments(dev):
@@ -223,7 +243,7 @@ def test_desc_base_and_empty_segments(dev):
             segs[j][-1] = frame(rng, 30)
     wire, so, sl = batch(segs, rng, gap=False)
     base = (np.arange(len(so), dtype=np.int64)[::-1] * 10).copy()
-    check(dev, wire, so, sl, 10, "desc_base", desc_base=base)
+    check(dev, wire, so, sl, 10, "desc_base", wirelen(333), desc_base=base)
 
 
 def test_state_across_calls_and_shapes(dev):
@@ -238,7 +258,7 @@ def test_state_across_calls_and_shapes(dev):
             if (j + i) % 2:
                 segs[j][j % 7 + 1] = frame(rng, 150)
         wire, so, sl = batch(segs, rng)
-        gb, gd, gr = check(dev, wire, so, sl, 8, "shape %d (%d)" % (i, nseg))
+        gb, gd, gr = check(dev, wire, so, sl, 8, "shape %d (%d)" % (i, nseg), wirelen(200))
         gb2, _, _ = P.gpu_decode(dev, gb.copy(), so, sl, 8)
         assert np.array_equal(gb2, wire), "decode twice"
 
@@ -248,6 +268,7 @@ def test_adaptive_choice(dev):
     advises the speculative path for a batch of equal frames; a batch of mixed lengths makes
     the repair kernel advise the scan kernel again. Every call bit-exact."""
     W.set_option("piece_spec", 1)
+    W.set_option("spec_g", 0)
     rng = np.random.default_rng(60)
     stream = torch.cuda.Stream(dev)
     uni = batch([[frame(rng, 2000) for _ in range(16)] for _ in range(200)], rng)

@@ -341,3 +341,38 @@ def test_reference_reactor_with_batch_glue(golden, tmp_path):
         assert v == tuple(_fixture_view(c)), c["name"]
         done += 1
     assert done >= 5
+
+
+def _batched_reactor_check(golden, chunk, gpu_fn=None, oracle_fn=None, max_frames=64):
+    """every fixture stream as one connection of a multi-connection batched reactor (grouped by
+    readcache_max_size): deliveries equal the reference reactor's own (the fixture)"""
+    import ref_reactor
+    from util_amd import load_lib
+    replay = C.cast(load_lib().websocketframeOnDecodeBatch, C.c_void_p).value
+    groups = {}
+    for c, wire in _reasm_cases(golden):
+        groups.setdefault(c["readcache_max"], []).append((c, wire))
+    total_batches = 0
+    for limit, cases in sorted(groups.items()):
+        res, nb = ref_reactor.reactor_deliver_batched([w for _, w in cases], chunk, limit, max_frames, gpu_fn=gpu_fn,
+                                                      oracle_fn=oracle_fn, replay_fn=replay)
+        total_batches += nb
+        for (c, _), r in zip(cases, res):
+            v = (r["lens"], _view_digest((r["lens"], r["bodies"], 0, 0, 0, 0, 0))[1], r["consumed"], r["frames"],
+                 r["detach_error"], r["pending"], r["cached"])
+            assert v == tuple(_fixture_view(c)), (c["name"], chunk)
+    return total_batches
+
+
+@pytest.mark.parametrize("chunk,max_frames", [(7, 64), (100, 64), (1500, 64), (65536, 64), (65536, 3)])
+def test_batched_reactor_binding_oracle(golden, chunk, max_frames):
+    """INTEGRATION.md §2 over the reference's own reactor and stream hook: recv for every
+    readable connection, ONE batch decode (here the oracle's, bit-identical to the GPU's) over
+    their whole inbufs — each starting with the previous read's undecoded tail — then each
+    connection's on_read loop replaying the batch through websocketframeOnDecodeBatch. The
+    streams arrive in `chunk`-byte writes, so frames and headers split across reads; a small
+    descriptor capacity makes the glue decode the frames past it on the host (MAX_FRAMES)."""
+    _reference_reactor()
+    olib = load_oracle()
+    fn = C.cast(olib.ws_oracle_decode_segments, C.c_void_p).value
+    assert _batched_reactor_check(golden, chunk, oracle_fn=fn, max_frames=max_frames) > 0

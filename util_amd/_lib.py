@@ -114,6 +114,8 @@ def load_lib():
                                                           vp]
     lib.websocketframeOnDecode.restype = None
     lib.websocketframeOnDecode.argtypes = [vp, vp, C.c_size_t, vp]
+    lib.websocketframeOnDecodeBatch.restype = None
+    lib.websocketframeOnDecodeBatch.argtypes = [vp, vp, C.c_size_t, vp]
     # launch tuning from the environment, e.g. WSFRAME_AMD_OPTIONS="path=0,seg_cfg=10"
     for kv in filter(None, os.environ.get("WSFRAME_AMD_OPTIONS", "").split(",")):
         name, _, value = kv.partition("=")

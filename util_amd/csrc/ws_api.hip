@@ -31,6 +31,7 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_spec_spins;
+WsOpt ws_spec_g{0};        // "spec_g": the frame length the speculative path predicts with (0: the device's hint)
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
 size_t ws_workspace_bytes_total();
@@ -105,6 +106,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_rounds")) {
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
+    }
+    else if (!strcmp(name, "spec_g")) {
+        if (value < 0 || value >= (1ll << 31) || value == 1) return -1;
+        ws_spec_g = (int)value;
     }
     else if (!strcmp(name, "spec_spins")) {
         if (value < 0 || value > (1 << 20)) return -1;
@@ -466,9 +471,11 @@ int WsSlot::spec(u64 span, u32 nseg, unsigned char** sws, u32* parity, u32* tag)
         w->spec_zero_nseg = nseg;                                   // fresh: heads + flags zeroed
         w->spec_dirty = false;
     }
-    if (w->spec_dirty && (e = hipMemsetAsync(w->sws, 0, 64, st)) != hipSuccess) return ws_set_err("spec reset", e);
+    if (w->spec_dirty && (e = hipMemsetAsync(w->sws, 0, ws_spec_flags_off(), st)) != hipSuccess)
+        return ws_set_err("spec reset", e);
     w->spec_dirty = false;
-    if (nseg > w->spec_zero_nseg && (e = hipMemsetAsync(w->sws + 64, 0, (size_t)nseg * 4, st)) != hipSuccess)
+    if (nseg > w->spec_zero_nseg &&
+        (e = hipMemsetAsync(w->sws + ws_spec_flags_off(), 0, (size_t)nseg * 4, st)) != hipSuccess)
         return ws_set_err("spec flags reset", e);
     w->spec_zero_nseg = nseg;           // flags past nseg may be overwritten by this call's list
     *sws = w->sws;
@@ -537,13 +544,16 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         if (!cap && (rc = slot.advice(&adv_h, &adv_d))) return rc;
         // speculative (no K1): eager calls only, when the checkers can cover the segment table,
         // and when the device advised it after the previous call on this slot (or forced)
-        if (!cap && spec_opt && ws_spec_fits(hi - lo, nseg) &&
+        // (the device's advice and frame-length hint: adv_h[0], adv_h[1]; option spec_g overrides the hint)
+        int hint = ws_spec_g > 0 ? (int)ws_spec_g : __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED);
+        if (spec_opt == 2 && hint < 2) hint = 1024;     // forced with no hint yet: any length verifies
+        if (!cap && spec_opt && hint >= 2 && ws_spec_fits(hi - lo, nseg) &&
             (spec_opt == 2 || __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1)) {
             unsigned char* sws = nullptr;
             u32 parity = 0, tag = 0;
             if ((rc = slot.spec(hi - lo, nseg, &sws, &parity, &tag))) return rc;
             ++ws_stat_spec_calls;
-            rc = ws_launch_piece_spec(L, lo, hi, sws, parity, tag, adv_d);
+            rc = ws_launch_piece_spec(L, lo, hi, sws, parity, tag, (u32)hint, adv_d);
             if (rc) slot.spec_failed();
             return rc;
         }

@@ -31,8 +31,18 @@ void websocketframeOnDecodeBatch(WebsocketBatchCursor_t* cur, unsigned char* buf
     WebsocketInbufDecodeResult_t* r = (WebsocketInbufDecodeResult_t*)result;
     const WebsocketFrameDesc_t* d;
     (void)len;
-    if (!cur || cur->next >= cur->res.n_frames) {        /* not decoded by the batch: keep as tail */
-        r->incomplete = 1;
+    if (!cur) { r->incomplete = 1; return; }
+    if (cur->next >= cur->res.n_frames) {
+        /* past the batch's frames: the reactor loop (net_reactor.c:515-526) goes on exactly as
+         * it would have without the GPU */
+        if (cur->res.status == WEBSOCKET_SEG_MAX_FRAMES) {
+            /* descriptor capacity ran out with frames left: decode them here, one per call */
+            websocketframeOnDecode(0, buf, len, result);
+        } else if (cur->res.status == WEBSOCKET_SEG_ERR_LEN_WRAP || cur->res.status == WEBSOCKET_SEG_ERR_DECODE) {
+            r->err = 1;                                   /* fenced wrap (the reference: UB) / ret < 0 */
+        } else {
+            r->incomplete = 1;                            /* an incomplete tail: kept for the next read */
+        }
         return;
     }
     d = cur->desc + cur->next;

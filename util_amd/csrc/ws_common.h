@@ -101,6 +101,24 @@ __device__ __forceinline__ void ws_hdr_from32(const u32x4 x0, const u32x4 x1, u3
     h1 = sh ? (a1 >> sh) | (a2 << (64 - sh)) : a1;
 }
 
+// The wire length of the batch's first frame (of the first segment with >= 2 bytes among the
+// first 8), 0 unless it is a plain complete frame: the speculative piece path's frame-length
+// hint for the next call on the stream (ws_spec.hip). One thread.
+__device__ __forceinline__ u32 ws_first_frame_len(const unsigned char* buf, const u64* seg_off, const u64* seg_len,
+                                                  u32 nseg) {
+    for (u32 s = 0; s < nseg && s < 8; ++s) {
+        const u64 so = seg_off[s], sl = seg_len[s];
+        if (sl < 2) continue;
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(buf + so);
+        const WS_GLOBAL u32x4* q = reinterpret_cast<const WS_GLOBAL u32x4*>(pa & ~(uintptr_t)15);
+        u64 h0, h1;
+        ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
+        const WsHdr h = ws_parse(h0, h1, sl);
+        return h.kind == WS_PARSE_FRAME && h.ret > 1 && (u64)h.hdr + h.plen == (u64)(u32)h.ret ? (u32)h.ret : 0u;
+    }
+    return 0;
+}
+
 // Descriptor as two 16-B stores (WebsocketFrameDesc_t layout).
 __device__ __forceinline__ void ws_store_desc(WebsocketFrameDesc_t* d, u64 frame_off, const WsHdr& h) {
     const u64 dof = h.plen ? frame_off + h.hdr : WEBSOCKET_DATA_OFF_NULL;
@@ -366,7 +384,9 @@ int ws_piece_dyn_lds(const WsLaunch& L);
 size_t ws_spec_workspace_bytes(u64 span, u32 nseg);
 size_t ws_spec_zero_bytes(u32 nseg);
 bool ws_spec_fits(u64 span, u32 nseg);
-int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, int* advice_dev);
+size_t ws_spec_flags_off();
+int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, u32 g,
+                         int* advice_dev);
 u32 ws_next_gen();
 int ws_device_info(int* cus, int* lds_per_cu);
 // auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are zero at allocation +

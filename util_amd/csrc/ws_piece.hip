@@ -316,6 +316,8 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         const u32 n = *gptr<u32>(nonuni);
         *gptr<u32>(nonuni) = 0;
         __hip_atomic_store(advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(advice + 1, (int)ws_first_frame_len(buf, seg_off, seg_len, nseg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -48,14 +48,19 @@ static_assert((1 << SPEC_RANGE_SHIFT) == 64 * SPEC_U * 16, "wave range");
 WsOpt ws_spec_spins{2048};
 
 enum { SPEC_CTR = 0, SPEC_NMIS = 1, SPEC_TMO = 2, SPEC_HEAD_WORDS = 4 };
+// the checkers' verdict, published by the last checker into SPEC_REPL words SPEC_REPL_STRIDE
+// bytes apart (every wave polls one of them: one word polled by a million waves is a memory
+// hot spot): 0 not yet, 1 ordered, 2 unordered
+#define SPEC_REPL 64
+#define SPEC_REPL_STRIDE 1024
 
 __device__ __forceinline__ u32 ld_agent(u32* p) {
     return __hip_atomic_load(gptr<u32>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // P = the number of segments whose offset is <= a, for ascending offsets (the segment
-// holding byte a, if any, is P - 1). Interpolation guess first (exact for uniform
-// segments), then 64-ary narrowing. Bounded on any input.
+// holding byte a, if any, is P - 1): a 64-entry window around the guess, then 64-ary
+// narrowing. Bounded on any input.
 __device__ __forceinline__ u32 spec_count_le(const u64* __restrict__ seg_off, u32 nseg, u64 a, u32 guess, u32 lane) {
     u32 lo = 0, hi = nseg;                       // off[s] <= a below lo, > a from hi (ascending input)
     {
@@ -84,29 +89,45 @@ __device__ __forceinline__ u32 spec_count_le(const u64* __restrict__ seg_off, u3
     return lo + (u32)__popcll(__ballot(i < hi && seg_off[i < nseg ? i : nseg - 1] <= a));
 }
 
-// The prediction for one segment from its first header (bytes never changed by any wave).
+// a wave-uniform value the compiler cannot prove uniform (e.g. computed in VALU): back to SGPRs
+__device__ __forceinline__ u64 uni64(u64 x) {
+    return (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)x) |
+           ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(x >> 32)) << 32);
+}
+__device__ __forceinline__ u32 uni32(u32 x) { return (u32)__builtin_amdgcn_readfirstlane((int)x); }
+
+// floor(x / g), wave-uniform, 2 <= g < 2^31, rg = 1.0f / g: an f32 estimate and at most two
+// corrections when x < 2^32 and the quotient < 2^20 (every frame count in practice), the
+// 64-bit division otherwise
+__device__ __forceinline__ u64 spec_div(u64 x, u64 g, float rg) {
+    if ((x >> 32) == 0 && x < (g << 20)) {
+        const u32 xx = (u32)x, dd = (u32)g;
+        u32 q = uni32((u32)((float)xx * rg));
+        long long r = (long long)xx - (long long)q * dd;
+        if (r < 0) { --q; r += dd; }
+        if (r < 0) { --q; r += dd; }
+        if (r >= (long long)dd) { ++q; r -= dd; }
+        if (r >= (long long)dd) { ++q; r -= dd; }
+        if (r >= 0 && r < (long long)dd) return q;
+    }
+    return uni64(x / g);
+}
+
+// The prediction for one segment of length sl: frames of wire length g back to back from
+// its start (g: the host's hint, the first frame length the previous call on the stream saw).
 struct SpecPred {
-    u64 g;           // predicted wire length of every frame (0: no frames predicted)
-    u32 n;           // frames predicted
+    u32 n;           // frames predicted: min(sl / g, max_frames)
     int status;      // predicted WEBSOCKET_SEG_* (OK or MAX_FRAMES)
     bool tail;       // the reference loop parses one more header (must be incomplete)
-    bool exact;      // false: the first frame is not a plain complete frame (walked exactly by S2)
 };
 
-__device__ __forceinline__ SpecPred spec_predict(const WsHdr& h0, u64 sl, u32 max_frames) {
+__device__ __forceinline__ SpecPred spec_predict(u64 sl, u64 g, float rg, u32 max_frames) {
     SpecPred p;
-    p.g = 0; p.n = 0; p.status = WEBSOCKET_SEG_OK; p.tail = false; p.exact = true;
-    if (sl < 2 || h0.kind == WS_PARSE_INCOMPLETE) return p;      // websocketframe.c:121-150: consumed 0
-    if (h0.kind == WS_PARSE_FRAME && h0.ret > 0 && (u64)h0.hdr + h0.plen == (u64)(u32)h0.ret) {
-        p.g = (u32)h0.ret;
-        const u64 q = sl / p.g;
-        p.n = q < max_frames ? (u32)q : max_frames;
-        const u64 used = (u64)p.n * p.g;
-        if (p.n == max_frames) p.status = used < sl ? WEBSOCKET_SEG_MAX_FRAMES : WEBSOCKET_SEG_OK;
-        else p.tail = sl - used >= 2;
-        return p;
-    }
-    p.exact = false;                                             // wrap fence, ret <= 0, (int) truncation
+    const u64 q = spec_div(sl, g, rg);
+    p.n = q < max_frames ? (u32)q : max_frames;
+    const u64 used = (u64)p.n * g;
+    p.status = p.n == max_frames && used < sl ? WEBSOCKET_SEG_MAX_FRAMES : WEBSOCKET_SEG_OK;
+    p.tail = p.n < max_frames && sl - used >= 2;
     return p;
 }
 
@@ -118,6 +139,17 @@ __device__ __forceinline__ WsHdr spec_header(const unsigned char* p, u64 avail) 
     u64 h0, h1;
     ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
     return ws_parse(h0, h1, avail);
+}
+
+// wave-uniform loads through the scalar path (lgkmcnt: they do not wait behind the wave's
+// payload loads, which vmcnt retires in order)
+typedef __attribute__((address_space(4))) const u64 cu64;
+__device__ __forceinline__ u64 sld64(const u64* p) { return *reinterpret_cast<cu64*>(reinterpret_cast<uintptr_t>(p)); }
+
+__device__ __forceinline__ WsHdr spec_parse_words(const HdrWords& hw, uintptr_t p, u64 avail) {
+    const u64 lo = (u64)hw.w0 | ((u64)hw.w1 << 32), mi = (u64)hw.w2 | ((u64)hw.w3 << 32), hi = (u64)hw.w4;
+    const u32 sh = 8u * (u32)(p & 3);
+    return ws_parse(sh ? (lo >> sh) | (mi << (64 - sh)) : lo, sh ? (mi >> sh) | (hi << (64 - sh)) : mi, avail);
 }
 
 __device__ __forceinline__ void spec_flag(u32* flags, u32* list, u32* head, u32 s) {
@@ -132,8 +164,9 @@ template <int NT>
 __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
-    WebsocketSegResult_t* __restrict__ res, u32* head, u32* flags, u32* list, u32* marks, u32 tag, u64 pbase,
-    u64 c_lo, u64 c_hi, u64 lo, u64 hi, u64 ppw, u64 npieces, u32 wshift, u32 nchk, u32 chk_per, u32 spins) {
+    WebsocketSegResult_t* __restrict__ res, u32* head, u32* done, u32* flags, u32* list, u32* marks, u32 tag,
+    u64 pbase, u64 c_lo, u64 c_hi, u64 lo, u64 hi, u64 ppw, u64 npieces, u32 wshift, u32 nchk, u32 chk_per,
+    u32 spins, u32 g32, float rg) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 bx = blockIdx.x;
@@ -150,9 +183,13 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
         const u64 c = wc0 + (u64)(u * 64 + lane);
         v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
     }
+    const u32 gw = bx * (SPEC_T / 64) + wv;
+    u32* const myrepl = done + (gw % SPEC_REPL) * (SPEC_REPL_STRIDE / 4);
+    // the checkers' verdict, polled now so the load is back by the stores (a wave that finds
+    // it not published yet polls again there)
+    u32 verdict = lane == 0 ? ld_agent(myrepl) : 0u;
     // ---- 2. checker duty (the first nchk waves): the segment table is ascending and inside
     //         [lo, hi) (the piece decomposition assumes it); zero-length results written here
-    const u32 gw = bx * (SPEC_T / 64) + wv;
     if (gw < nchk) {
         const u64 s_beg = (u64)gw * chk_per;
         const u64 s_end = s_beg + chk_per < nseg ? s_beg + chk_per : nseg;
@@ -167,38 +204,54 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
             }
         }
         const bool any = __ballot(bad) != 0;
+        u32 old = 0;
         if (lane == 0)
-            __hip_atomic_fetch_add(gptr<u32>(head + SPEC_CTR), 1u + (any ? 0x10000u : 0u), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            old = __hip_atomic_fetch_add(gptr<u32>(head + SPEC_CTR), 1u + (any ? 0x10000u : 0u), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        old = (u32)__builtin_amdgcn_readlane((int)old, 0);
+        if ((old & 0xFFFFu) + 1 == nchk) {       // the last checker publishes the verdict
+            const u32 vd = ((old >> 16) || any) ? 2u : 1u;
+            __hip_atomic_store(gptr<u32>(done + lane * (SPEC_REPL_STRIDE / 4)), vd, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     constexpr long long RW = 64 * SPEC_U * 16;                              // this wave's bytes
     const u64 r0 = wc0 << 4, r1 = r0 + RW;                                  // origin-relative
     const u64 ra = r0 > lead0 ? r0 - lead0 : 0, rb = r1 - lead0;            // buffer-relative
     const int xl = (int)lane * 16;
+    const u64 g = g32;
     u32 cov[SPEC_U], segcov[SPEC_U];
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) { cov[u] = 0; segcov[u] = 0; }
     u32 s_first = 0, s_stop = 0;                                            // segments visited [s_first, s_stop)
-    bool gave_up = false;
     if (pvalid) {
         // ---- 3. the segments under [ra, rb): the last one starting at or before ra, then on
-        const u64 first = seg_off[0], last_end = seg_off[nseg - 1] + seg_len[nseg - 1];
+        const u64 first = sld64(seg_off), last_end = sld64(seg_off + nseg - 1) + sld64(seg_len + nseg - 1);
         u32 guess = 0;
-        if (ra > first && last_end > first) {
-            const double f = (double)(ra - first) / (double)(last_end - first);
-            guess = f >= 1.0 ? nseg - 1 : (u32)(f * (double)nseg);
-            if (guess >= nseg) guess = nseg - 1;
+        if (ra > first && last_end > first) {   // (f32 is exact enough: the guess is checked)
+            const float f = (float)(ra - first) * __builtin_amdgcn_rcpf((float)(last_end - first));
+            guess = f >= 1.0f ? nseg - 1 : (u32)(f * (float)nseg);
+            guess = uni32(guess < nseg ? guess : nseg - 1);
         }
-        const u32 P = spec_count_le(seg_off, nseg, ra, guess, lane);
-        u32 s = P ? P - 1 : 0;
+        u32 s;
+        {   // the guess, checked by two scalar loads (uniform segments: always right)
+            const u64 o0 = sld64(seg_off + guess), o1 = guess + 1 < nseg ? sld64(seg_off + guess + 1) : ~0ull;
+            if ((o0 <= ra && ra < o1) || (guess == 0 && ra < o0)) {
+                s = guess;
+            } else {
+                const u32 P = spec_count_le(seg_off, nseg, ra, guess, lane);
+                s = P ? P - 1 : 0;
+            }
+        }
         s_first = s;
         for (u32 it = 1; s < nseg; ++s, ++it) {
             if ((it & 63) == 0) {                                           // an unordered batch stores nothing:
-                u32 c = lane == 0 ? ld_agent(head + SPEC_CTR) : 0u;         // stop walking garbage early
-                if (__builtin_amdgcn_readfirstlane(c) >> 16) break;
+                const u32 cc = lane == 0 ? ld_agent(myrepl) : 0u;           // stop walking garbage early
+                if (__builtin_amdgcn_readfirstlane(cc) == 2) break;
             }
-            const u64 so = seg_off[s], sl = seg_len[s];
+            s = uni32(s);
+            const u64 so = uni64(sld64(seg_off + s)), sl = uni64(sld64(seg_len + s));
             if (so >= rb) break;
             if (sl == 0 || (so < ra && sl <= ra - so)) continue;           // empty, or ends before the range
             if (so > hi || sl > hi - so) {                                  // outside the batch: the checkers
@@ -218,88 +271,75 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                     if (h2 > l2) segcov[u] |= (0xFFFFu >> (16 - h2)) & (0xFFFFu << l2);
                 }
             }
-            const WsHdr h0 = spec_header(buf + so, sl);
-            const SpecPred pr = spec_predict(h0, sl, max_frames);
-            bool bad = !pr.exact;
+            const SpecPred pr = spec_predict(sl, g, rg, max_frames);
+            bool bad = false;
             if (lane == 0 && sorg >= r0 && sorg < r1)                       // result: the wave holding byte 0
-                ws_store_res(res + s, (u64)pr.n * pr.g, pr.n, pr.status);
+                ws_store_res(res + s, (u64)pr.n * g, pr.n, pr.status);
             const u64 kend = (u64)pr.n + (pr.tail ? 1u : 0u);               // + the tail header to check
-            if (kend) {
-                const u64 g = pr.g;
-                const u64 kA = r0 > sorg ? (r0 - sorg) / g : 0;              // frame holding r0
-                u64 kB = (r1 - sorg + g - 1) / g;                           // frames starting before r1
-                if (kB > kend) kB = kend;
-                const u64 dbase = desc_base ? desc_base[s] : (u64)s * max_frames;
-                for (u64 kk = kA; kk < kB; kk += 64) {
-                    const u64 k = kk + lane;
-                    const bool act = k < kB;
-                    const u64 kc = act ? k : kA;
-                    const u64 pos = so + kc * g;
-                    const WsHdr h = spec_header(buf + pos, sl - kc * g);
-                    const u64 porg = pos + lead0;
-                    const bool tail = act && pr.tail && k == pr.n;
-                    bool b = false;
-                    if (act && porg >= r0 && porg < r1) {                   // this wave owns the header
-                        if (tail) b = h.kind != WS_PARSE_INCOMPLETE;
-                        else if (h.kind == WS_PARSE_FRAME && (u64)h.hdr + h.plen == g) ws_store_desc(desc + dbase + k, pos, h);
-                        else b = true;
-                    }
-                    if (__ballot(b)) bad = true;
-                    // the XOR rule (see the top of the file)
-                    const bool x = act && !tail && h.kind == WS_PARSE_FRAME && h.masked && h.hdr < g;
-                    const u64 p0 = porg + h.hdr, p1 = porg + g;
-                    const long long qa = (long long)(p0 - r0), qb = (long long)(p1 - r0);
-                    const int A = (int)(qa < -16 ? -16 : (qa > RW + 16 ? RW + 16 : qa));
-                    const int B = (int)(qb < -16 ? -16 : (qb > RW + 16 ? RW + 16 : qb));
-                    const u32 rk = rotl32(h.key, 8u * (u32)(p0 & 3));
-                    u64 hm = __ballot(x && p1 > r0 && p0 < r1);
-                    while (hm) {
-                        const int i = __builtin_ctzll(hm);
-                        hm &= hm - 1;
-                        const int a = __builtin_amdgcn_readlane(A, i), bb = __builtin_amdgcn_readlane(B, i);
-                        const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
+            const u64 kA = uni64(r0 > sorg ? spec_div(r0 - sorg, g, rg) : 0);    // frame holding r0
+            u64 kB = spec_div(r1 - sorg + g - 1, g, rg);                    // frames starting before r1
+            kB = uni64(kB > kend ? kend : kB);
+            const u64 dbase = uni64(desc_base ? sld64(desc_base + s) : (u64)s * max_frames);
+            // one scalar header load per frame, the next one issued before the current one is
+            // parsed (1-2 frames per 4 KiB range at cfg2's frames)
+            const u32 nfr = uni32(kB > kA ? (u32)(kB - kA) : 0u);
+            HdrWords hn = load_header(buf + uni64(so + kA * g));
+            for (u32 i = 0; i < nfr; ++i) {
+                const u64 k = uni64(kA + i);
+                const u64 pos = uni64(so + k * g);
+                const HdrWords hc = hn;
+                if (i + 1 < nfr) hn = load_header(buf + uni64(pos + g));
+                const WsHdr h = spec_parse_words(hc, reinterpret_cast<uintptr_t>(buf) + pos, sl - k * g);
+                const u64 porg = pos + lead0;
+                const bool tail = pr.tail && k == pr.n;
+                if (porg >= r0 && porg < r1) {                              // this wave owns the header
+                    if (tail) bad |= h.kind != WS_PARSE_INCOMPLETE;
+                    else if (h.kind == WS_PARSE_FRAME && (u64)h.hdr + h.plen == g) {
+                        if (lane == 0) ws_store_desc(desc + dbase + k, pos, h);
+                    } else bad = true;
+                }
+                if (tail || h.kind != WS_PARSE_FRAME || !h.masked || h.hdr >= g) continue;   // the XOR rule
+                const u64 p0 = porg + h.hdr, p1 = porg + g;
+                if (p1 <= r0 || p0 >= r1) continue;
+                const long long qa = (long long)(p0 - r0), qb = (long long)(p1 - r0);
+                const int a = (int)(qa < -16 ? -16 : (qa > RW + 16 ? RW + 16 : qa));
+                const int bb = (int)(qb < -16 ? -16 : (qb > RW + 16 ? RW + 16 : qb));
+                const u32 key = rotl32(h.key, 8u * (u32)(p0 & 3));
 #pragma unroll
-                        for (int u = 0; u < SPEC_U; ++u) {
-                            if (bb <= u * 1024 || a >= u * 1024 + 1024) continue;   // (uniform) not in row u
-                            const int xx = u * 1024 + xl;
-                            const int l2 = a > xx ? a - xx : 0, h2 = bb < xx + 16 ? bb - xx : 16;
-                            if (h2 <= l2) continue;
-                            ws_xor_range(key, l2, h2, v[u], cov[u]);
-                        }
-                    }
+                for (int u = 0; u < SPEC_U; ++u) {
+                    if (bb <= u * 1024 || a >= u * 1024 + 1024) continue;       // (uniform) not in row u
+                    const int xx = u * 1024 + xl;
+                    const int l2 = a > xx ? a - xx : 0, h2 = bb < xx + 16 ? bb - xx : 16;
+                    if (h2 <= l2) continue;
+                    ws_xor_range(key, l2, h2, v[u], cov[u]);
                 }
             }
             if (bad && lane == 0) spec_flag(flags, list, head, s);
         }
         s_stop = s < nseg ? s + 1 : nseg;
     }
-    // ---- 4. wait for the checkers (bounded), then store
-    u32 c = 0;
+    // ---- 4. wait for the checkers' verdict (bounded), then store
     if (lane == 0) {
-        c = ld_agent(head + SPEC_CTR);
-        for (u32 n = 0; (c & 0xFFFFu) < nchk && n < spins; ++n) {
+        for (u32 n = 0; verdict == 0 && n < spins; ++n) {
             __builtin_amdgcn_s_sleep(2);
-            c = ld_agent(head + SPEC_CTR);
+            verdict = ld_agent(myrepl);
         }
     }
-    c = (u32)__builtin_amdgcn_readlane((int)c, 0);
-    const bool unordered = (c >> 16) != 0;
-    if (!pvalid || unordered) return;                                       // S2 walks an unordered batch
-    if ((c & 0xFFFFu) < nchk) {
+    verdict = (u32)__builtin_amdgcn_readlane((int)verdict, 0);
+    if (!pvalid || verdict == 2) return;                                    // S2 walks an unordered batch
+    if (verdict == 0) {
         // gave up waiting: store nothing; S2 finishes this range's segments (their XOR is
         // undone on the ranges that did store, then they are walked exactly)
-        gave_up = true;
         if (lane == 0) {
             *gptr<u32>(marks + ((r0 >> SPEC_RANGE_SHIFT) - (pbase << (SPEC_SHIFT - SPEC_RANGE_SHIFT)))) = tag;
             __hip_atomic_fetch_add(gptr<u32>(head + SPEC_TMO), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (u32 s = s_first; s < s_stop; ++s) {
-                const u64 so = seg_off[s], sl = seg_len[s];
+                const u64 so = sld64(seg_off + s), sl = sld64(seg_len + s);
                 if (sl && !(so < ra && sl <= ra - so) && so < rb) spec_flag(flags, list, head, s);
             }
         }
         return;
     }
-    (void)gave_up;
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) {
         const u64 cidx = wc0 + (u64)(u * 64 + lane);
@@ -372,14 +412,15 @@ template <int NT>
 __global__ __launch_bounds__(256) void ws_piece_spec_fix_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
-    WebsocketSegResult_t* __restrict__ res, const u32* head, u32* next_head, u32* flags, const u32* list,
-    const u32* marks, u32 tag, u64 pbase, int* advice) {
+    WebsocketSegResult_t* __restrict__ res, const u32* head, u32* next_head, u32* next_done, u32* flags,
+    const u32* list, const u32* marks, u32 tag, u64 pbase, u32 g32, float rg, int* advice) {
     const u32 lane = threadIdx.x & 63;
     const u32 gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u32 nw = gridDim.x * 4;
     const u32 c = *gptr<u32>(head + SPEC_CTR), nmis = *gptr<u32>(head + SPEC_NMIS);
     const bool tmo = *gptr<u32>(head + SPEC_TMO) != 0;
     const u64 rbase = pbase << (SPEC_SHIFT - SPEC_RANGE_SHIFT);
+    const u64 g = g32;
     if (c >> 16) {
         // unordered (or outside [lo, hi)): S1 stored nothing; the reactor loop per segment
         for (u32 s = gw; s < nseg; s += nw) spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
@@ -388,45 +429,55 @@ __global__ __launch_bounds__(256) void ws_piece_spec_fix_kernel(
         for (u32 i = gw; i < nmis; i += nw) {
             const u32 s = list[i];
             const u64 so = seg_off[s], sl = seg_len[s];
-            const WsHdr h0 = spec_header(buf + so, sl);
-            const SpecPred pr = spec_predict(h0, sl, max_frames);
+            const SpecPred pr = spec_predict(sl, g, rg, max_frames);
             for (u32 k = 0; k < pr.n; ++k) {                           // undo S1's XOR where it stored
-                unsigned char* const p = buf + so + (u64)k * pr.g;
-                const WsHdr h = spec_header(p, sl - (u64)k * pr.g);
-                if (h.kind == WS_PARSE_FRAME && h.masked && h.hdr < pr.g)
-                    spec_xor_stored<NT>(buf, p + h.hdr, p + pr.g, h.key, marks, tag, rbase, tmo, lane);
+                unsigned char* const p = buf + so + (u64)k * g;
+                const WsHdr h = spec_header(p, sl - (u64)k * g);
+                if (h.kind == WS_PARSE_FRAME && h.masked && h.hdr < g)
+                    spec_xor_stored<NT>(buf, p + h.hdr, p + g, h.key, marks, tag, rbase, tmo, lane);
             }
             spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
             if (lane == 0) *gptr<u32>(flags + s) = 0;
         }
     }
-    if (gw == 0 && lane == 0) {
-        // the next call's head rests at zero; advice for the host's next path choice: stay
-        // speculative while at most 1/32 of the segments needed the exact walk
-        gu32* nh = gptr<u32>(next_head);
-        nh[SPEC_CTR] = 0;
-        nh[SPEC_NMIS] = 0;
-        nh[SPEC_TMO] = 0;
-        if (advice)
-            __hip_atomic_store(advice, (c >> 16) == 0 && (u64)nmis * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+    if (gw == 0) {
+        // the next call's head and verdict words rest at zero
+        gptr<u32>(next_done)[lane * (SPEC_REPL_STRIDE / 4)] = 0;
+        if (lane == 0) {
+            gu32* nh = gptr<u32>(next_head);
+            nh[SPEC_CTR] = 0;
+            nh[SPEC_NMIS] = 0;
+            nh[SPEC_TMO] = 0;
+            // the host's next path choice: stay speculative while at most 1/32 of the segments
+            // needed the exact walk; the frame length to predict with next time
+            if (advice) {
+                __hip_atomic_store(advice, (c >> 16) == 0 && (u64)nmis * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(advice + 1, (int)ws_first_frame_len(buf, seg_off, seg_len, nseg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------
 extern WsOpt ws_piece_win;
-extern WsOpt ws_piece_lds;
 extern WsOpt ws_k2_timing;
 int ws_k2_mark(hipStream_t st, bool end, size_t* slot);
 
-// spec workspace: [head A: 4 u32][head B: 4 u32][pad to 64][flags: nseg u32][list: nseg u32][marks: ranges u32]
+// spec workspace: [head A, head B: 4 u32 each][verdict words A, B: SPEC_REPL x SPEC_REPL_STRIDE each]
+//                 [flags: nseg u32][list: nseg u32][marks: one u32 per 4 KiB range]
+#define SPEC_OFF_DONE 1024
+#define SPEC_DONE_BYTES (SPEC_REPL * SPEC_REPL_STRIDE)
+size_t ws_spec_flags_off() { return SPEC_OFF_DONE + 2 * SPEC_DONE_BYTES; }
+
 size_t ws_spec_workspace_bytes(u64 span, u32 nseg) {
     const u64 ranges = ((span + 15) >> SPEC_RANGE_SHIFT) + 8;
-    return 64 + (size_t)nseg * 8 + (size_t)ranges * 4 + 64;
+    return ws_spec_flags_off() + (size_t)nseg * 8 + (size_t)ranges * 4 + 64;
 }
 
-// bytes that must be zero when the workspace is (re)allocated: heads + flags
-size_t ws_spec_zero_bytes(u32 nseg) { return 64 + (size_t)nseg * 4; }
+// bytes that must be zero when the workspace is (re)allocated: heads, verdict words, flags
+size_t ws_spec_zero_bytes(u32 nseg) { return ws_spec_flags_off() + (size_t)nseg * 4; }
 
 // S1 can run only when its checkers are a small part of the grid: <= 1024 waves of <= 256 segments
 bool ws_spec_fits(u64 span, u32 nseg) {
@@ -436,15 +487,20 @@ bool ws_spec_fits(u64 span, u32 nseg) {
     return npieces >= 1 && nseg >= 1 && (u64)nseg <= nchk * 256;
 }
 
-int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, int* advice_dev) {
+// g: the frame wire length to predict every segment with (>= 2)
+int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, u32 g,
+                         int* advice_dev) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     const u64 npieces = hi_org > lo_org ? ((hi_org - 1) >> SPEC_SHIFT) - (lo_org >> SPEC_SHIFT) + 1 : 0;
-    if (!npieces) return ws_set_msg("spec decode: empty range");
+    if (!npieces || g < 2 || g >= (1u << 31)) return ws_set_msg("spec decode: empty range or no frame length");
     const u64 pbase = lo_org >> SPEC_SHIFT, c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
-    u32* head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * (parity & 1);
-    u32* next_head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * ((parity + 1) & 1);
-    u32* flags = reinterpret_cast<u32*>(sws + 64);
+    const u32 p = parity & 1;
+    u32* head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * p;
+    u32* next_head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * (p ^ 1);
+    u32* done = reinterpret_cast<u32*>(sws + SPEC_OFF_DONE + p * SPEC_DONE_BYTES);
+    u32* next_done = reinterpret_cast<u32*>(sws + SPEC_OFF_DONE + (p ^ 1) * SPEC_DONE_BYTES);
+    u32* flags = reinterpret_cast<u32*>(sws + ws_spec_flags_off());
     u32* list = flags + L.nseg;
     u32* marks = list + L.nseg;
     const int pwin = ws_piece_win;
@@ -456,22 +512,22 @@ int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, 
     const u32 nchk = (u32)(waves < 1024 ? waves : 1024);
     const u32 chk_per = (u32)((L.nseg + nchk - 1) / nchk);
     if (chk_per > 256) return ws_set_msg("spec decode: too many segments for the checkers");
+    const float rg = 1.0f / (float)g;
     size_t tslot = 0;
     int rc;
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    const int dyn = ws_piece_lds;
-    hipLaunchKernelGGL(ws_piece_spec_kernel<1>, dim3((u32)grid), dim3(SPEC_T), dyn > 0 && dyn <= 65536 ? dyn : 0,
-                       L.stream, L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head,
-                       flags, list, marks, tag, pbase, c_lo, c_hi, lo, hi, ppw, npieces, wshift, nchk, chk_per,
-                       (u32)(int)ws_spec_spins);
+    hipLaunchKernelGGL(ws_piece_spec_kernel<1>, dim3((u32)grid), dim3(SPEC_T), ws_piece_dyn_lds(L), L.stream, L.buf,
+                       L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, done, flags, list,
+                       marks, tag, pbase, c_lo, c_hi, lo, hi, ppw, npieces, wshift, nchk, chk_per,
+                       (u32)(int)ws_spec_spins, g, rg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_spec_kernel launch", e);
     if (timing && (rc = ws_k2_mark(L.stream, true, &tslot))) return rc;
     const u32 fix_blocks = (u32)((L.nseg + 3) / 4 < 256 ? (L.nseg + 3) / 4 : 256);
     hipLaunchKernelGGL(ws_piece_spec_fix_kernel<1>, dim3(fix_blocks), dim3(256), 0, L.stream, L.buf, L.seg_off,
-                       L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, next_head, flags, list,
-                       marks, tag, pbase, advice_dev);
+                       L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, next_head, next_done, flags,
+                       list, marks, tag, pbase, g, rg, advice_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_spec_fix_kernel launch", e);
     return 0;
