@@ -194,3 +194,54 @@ def test_first_library_call_inside_capture(dev):
     r = subprocess.run([sys.executable, "-c", FIRST_CALL, here, os.path.dirname(here)], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("kind", ["batch", "stream"])
+def test_capture_workspaces_released_with_their_graphs(dev, kind):
+    """every graph capture gets workspaces of its own; destroying the graph (and its
+    executable) releases them (a HIP user object on the captured graph): 50 captures made and
+    destroyed leave the library's device workspace where one capture leaves it"""
+    import gc
+    import time
+    rng = np.random.default_rng(43)
+    wire, so, sl = random_stream(rng, 300)
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    d[:n].copy_(torch.from_numpy(wire).to(dev))
+    so_t = torch.tensor(so, dtype=torch.int64, device=dev)
+    sl_t = torch.tensor(sl, dtype=torch.int64, device=dev)
+    desc = torch.zeros(max(len(so), n // 2 + 1) * 16 * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
+
+    def call():
+        if kind == "batch":
+            W.batch_decode_device(d, so_t, sl_t, 16, desc, res)
+        else:
+            W.stream_decode_device(d, n, n // 2 + 1, desc, res)
+
+    def settle():                     # user-object destructors may run a little later
+        for _ in range(50):
+            gc.collect()
+            call()                    # a library call frees the slots of destroyed graphs
+            torch.cuda.synchronize()
+            time.sleep(0.02)
+        return W.get_stat("workspace_bytes")
+
+    call()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        call()
+    g.replay()
+    torch.cuda.synchronize()
+    del g
+    one = settle()
+    for _ in range(50):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            call()
+        g.replay()
+        torch.cuda.synchronize()
+        del g
+    after = settle()
+    assert after <= one, (one, after)

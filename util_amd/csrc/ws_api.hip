@@ -30,7 +30,7 @@ extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
-extern WsOpt ws_spec_spins;
+extern WsOpt ws_spec_spins, ws_spec_dbg;
 WsOpt ws_spec_g{0};        // "spec_g": the frame length the speculative path predicts with (0: the device's hint)
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
@@ -107,6 +107,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
     }
+    else if (!strcmp(name, "spec_dbg")) ws_spec_dbg = (int)value;
     else if (!strcmp(name, "spec_g")) {
         if (value < 0 || value >= (1ll << 31) || value == 1) return -1;
         ws_spec_g = (int)value;
@@ -547,7 +548,7 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         // (the device's advice and frame-length hint: adv_h[0], adv_h[1]; option spec_g overrides the hint)
         int hint = ws_spec_g > 0 ? (int)ws_spec_g : __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED);
         if (spec_opt == 2 && hint < 2) hint = 1024;     // forced with no hint yet: any length verifies
-        if (!cap && spec_opt && hint >= 2 && ws_spec_fits(hi - lo, nseg) &&
+        if (!cap && spec_opt && hint >= 2 && hint < (1 << 30) && ws_spec_fits(hi - lo, nseg) &&
             (spec_opt == 2 || __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1)) {
             unsigned char* sws = nullptr;
             u32 parity = 0, tag = 0;

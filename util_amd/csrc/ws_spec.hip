@@ -7,35 +7,39 @@
 //
 // S1 ws_piece_spec_kernel — one 256-thread block per 16 KiB piece (K2's block shape,
 //   windows and stores). Each wave issues its payload loads, then finds the segments
-//   under its 4 KiB range (interpolation guess + 64-lane window on seg_off), reads each
-//   segment's FIRST header and predicts the frame grid so + k*g (g = that frame's wire
-//   length), parses the predicted headers that touch its range (the bytes it streams
-//   anyway, one 32-B line per frame) and XORs each frame's payload with its own key.
-//   The wave holding a predicted header verifies it (complete frame of length exactly g;
-//   after the last predicted frame an incomplete tail) and writes its descriptor; the
-//   wave holding the segment's first byte writes the predicted segment result. A
-//   mismatch flags the segment (one atomicOr per segment, the first flagger appends it to
-//   a list). The first `nchk` waves of the grid also check the segment table (ascending,
-//   inside [lo, hi)) and count themselves done on an agent-scope counter; every wave
-//   polls that counter (relaxed, bounded spin) before its stores: an unordered batch
-//   stores nothing, and a wave that gives up waiting stores nothing, tags its range and
-//   flags its segments (results never depend on dispatch order, only speed does).
+//   under its 4 KiB range (an interpolation guess checked by two scalar loads) and
+//   predicts every segment as frames of ONE wire length g back to back from its start —
+//   g is the host's hint: the first frame length the previous call on the stream saw.
+//   Per predicted frame k at so + k*g the wave checks the header against the header
+//   signature of a complete frame of length g (host-computed: for each length form and
+//   MASK bit, the expected byte 1 / extended length, websocketframe.c:126-150) — a
+//   scalar load and a few compares — and XORs the payload of every frame that matches
+//   with its key. The wave holding a header verifies it for the segment (a mismatch,
+//   or after the last predicted frame a header that is not incomplete, flags the
+//   segment: one atomicOr, the first flagger lists it) and writes its descriptor; the
+//   wave holding the segment's first byte writes the predicted segment result. The first
+//   `nchk` waves also check the segment table (ascending, inside [lo, hi)); the last of
+//   them publishes the verdict into replicated words, which every wave polls (relaxed,
+//   bounded) before its stores: an unordered batch stores nothing, a wave that gives up
+//   waiting stores nothing, tags its range and flags its segments (results never depend
+//   on dispatch order, only speed does).
 // S2 ws_piece_spec_fix_kernel — tiny unless something was flagged: unordered batch ->
-//   every segment walked exactly (ws_walk.h); flagged segments -> the speculative XOR
-//   undone (XOR is an involution; the same rule over the same header bytes) on the ranges
-//   that stored, then walked exactly.
+//   every segment walked exactly; flagged segments -> the speculative XOR undone (XOR is
+//   an involution; the same rule over the same header bytes) on the ranges that stored,
+//   then walked exactly (net_reactor.c:515-526 over websocketframeDecode).
 //
-// Why the speculation is race-free: for predicted frame k at pos = so + k*g the XOR
-// rule is "frame parses (avail = sl - k*g), MASK set, hdr < g: XOR [pos + hdr, pos + g)
-// with its key". Every input of that rule (bytes 1 and the ext length / key bytes, all in
-// [pos, pos + hdr)) lies outside every XOR range, so all waves (and S2's undo) read the
-// same original bytes whatever has been stored; for hdr >= g the rule is "no XOR"
-// whatever the other bytes hold. A verified frame has hdr + plen == g, so the rule then
-// is exactly the reference's unmask (websocketframe.c:153-158).
+// Why the speculation is race-free: for predicted frame k at pos = so + k*g the rule is
+// "the header matches the signature of form (byte 1) and MASK: XOR [pos + hdr, pos + g)
+// with its key". A form whose header would be longer than g never matches (decided from
+// byte 1 alone); otherwise every byte the rule reads lies in [pos, pos + hdr) — outside
+// every XOR range — so all waves (and S2's undo) read the original bytes whatever has
+// been stored. A matching header is a complete frame of total length g (websocketframe.c
+// :149 with avail >= g; g < 2^31, no wrap), so the rule is the reference's unmask
+// (:153-158) and the descriptor its out-params.
 //
-// State (per workspace slot, parity-double-buffered head, see ws_api.hip): head words
-// {ctr, nmis, tmo} rest at zero; S2 of call i zeroes the head of call i + 1; S2 clears
-// the flags it consumed. Not used inside HIP graph captures (the host picks the path).
+// State (per workspace slot, parity-double-buffered, see ws_api.hip): head words
+// {ctr, nmis, tmo} and the verdict words rest at zero; S2 of call i zeroes those of call
+// i + 1 and clears the flags it consumed. Not used inside HIP graph captures.
 #include "ws_walk.h"
 
 #define SPEC_T 256
@@ -46,6 +50,7 @@ static_assert((1 << SPEC_RANGE_SHIFT) == 64 * SPEC_U * 16, "wave range");
 // bounded wait for the checkers (s_sleep 2 + a load each): option "spec_spins" (0 = give up
 // unless the first poll finds them done: exercises the repair path in tests)
 WsOpt ws_spec_spins{2048};
+WsOpt ws_spec_dbg{0};     // TEMPORARY: instruction-count experiments
 
 enum { SPEC_CTR = 0, SPEC_NMIS = 1, SPEC_TMO = 2, SPEC_HEAD_WORDS = 4 };
 // the checkers' verdict, published by the last checker into SPEC_REPL words SPEC_REPL_STRIDE
@@ -53,6 +58,51 @@ enum { SPEC_CTR = 0, SPEC_NMIS = 1, SPEC_TMO = 2, SPEC_HEAD_WORDS = 4 };
 // hot spot): 0 not yet, 1 ordered, 2 unordered
 #define SPEC_REPL 64
 #define SPEC_REPL_STRIDE 1024
+
+// The header signature of a complete frame of wire length g (host-computed, by value): per
+// MASK bit m, what byte 1 and the extended length must hold (websocketframe.c:126-150).
+struct SpecSig {
+    u32 g;
+    u32 b1[2];        // 7-bit form: byte 1 exactly (0x100: g does not fit this form)
+    u32 e16[2];       // 16-bit form: bytes 2-3 read little-endian (0x10000: impossible)
+    u32 ok64[2];      // the 64-bit form is possible (g >= 10 + 4m)
+    float rg;         // 1.0f / g
+    u64 e64[2];       // 64-bit form: bytes 2-9 read little-endian
+};
+
+static SpecSig spec_sig(u32 g) {
+    SpecSig S;
+    S.g = g;
+    S.rg = 1.0f / (float)g;
+    for (u32 m = 0; m < 2; ++m) {
+        const u32 h7 = 2 + 4 * m, h16 = 4 + 4 * m, h64 = 10 + 4 * m;
+        S.b1[m] = g >= h7 && g - h7 < 126 ? ((m << 7) | (g - h7)) : 0x100u;
+        S.e16[m] = g >= h16 && g - h16 <= 0xFFFF ? (((g - h16) >> 8) | (((g - h16) & 0xFFu) << 8)) : 0x10000u;
+        S.ok64[m] = g >= h64;
+        S.e64[m] = g >= h64 ? __builtin_bswap64((u64)(g - h64)) : 0;
+    }
+    return S;
+}
+
+// The frame at a predicted position: header bytes 0..15 as w0, w1 (little-endian, uniform).
+// true: a complete frame of length g — hdr, masked, key (wire order) set.
+__device__ __forceinline__ bool spec_match(u64 w0, u64 w1, const SpecSig& S, u32& hdr, u32& masked, u32& key) {
+    const u32 b1 = (u32)(w0 >> 8) & 0xFFu, m = b1 >> 7, p7 = b1 & 0x7Fu;
+    masked = m;
+    if (p7 < 126) {
+        hdr = 2 + 4 * m;
+        key = (u32)(w0 >> 16);
+        return b1 == S.b1[m];
+    }
+    if (p7 == 126) {
+        hdr = 4 + 4 * m;
+        key = (u32)(w0 >> 32);
+        return ((u32)(w0 >> 16) & 0xFFFFu) == S.e16[m];
+    }
+    hdr = 10 + 4 * m;
+    key = (u32)(w1 >> 16);
+    return S.ok64[m] && ((w0 >> 16) | (w1 << 48)) == S.e64[m];
+}
 
 __device__ __forceinline__ u32 ld_agent(u32* p) {
     return __hip_atomic_load(gptr<u32>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -113,43 +163,25 @@ __device__ __forceinline__ u64 spec_div(u64 x, u64 g, float rg) {
     return uni64(x / g);
 }
 
-// The prediction for one segment of length sl: frames of wire length g back to back from
-// its start (g: the host's hint, the first frame length the previous call on the stream saw).
-struct SpecPred {
-    u32 n;           // frames predicted: min(sl / g, max_frames)
-    int status;      // predicted WEBSOCKET_SEG_* (OK or MAX_FRAMES)
-    bool tail;       // the reference loop parses one more header (must be incomplete)
-};
-
-__device__ __forceinline__ SpecPred spec_predict(u64 sl, u64 g, float rg, u32 max_frames) {
-    SpecPred p;
-    const u64 q = spec_div(sl, g, rg);
-    p.n = q < max_frames ? (u32)q : max_frames;
-    const u64 used = (u64)p.n * g;
-    p.status = p.n == max_frames && used < sl ? WEBSOCKET_SEG_MAX_FRAMES : WEBSOCKET_SEG_OK;
-    p.tail = p.n < max_frames && sl - used >= 2;
-    return p;
-}
-
-// header of the frame at byte p (vector loads: WEBSOCKET_BATCH_PAD makes the 32 B readable)
-__device__ __forceinline__ WsHdr spec_header(const unsigned char* p, u64 avail) {
-    const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
-    const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-    const u32x4 x0 = q[0], x1 = q[1];
-    u64 h0, h1;
-    ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
-    return ws_parse(h0, h1, avail);
-}
-
 // wave-uniform loads through the scalar path (lgkmcnt: they do not wait behind the wave's
 // payload loads, which vmcnt retires in order)
 typedef __attribute__((address_space(4))) const u64 cu64;
 __device__ __forceinline__ u64 sld64(const u64* p) { return *reinterpret_cast<cu64*>(reinterpret_cast<uintptr_t>(p)); }
 
-__device__ __forceinline__ WsHdr spec_parse_words(const HdrWords& hw, uintptr_t p, u64 avail) {
+// header bytes [p, p + 16) by vector loads (WEBSOCKET_BATCH_PAD makes the 32 B readable)
+__device__ __forceinline__ void spec_words_v(const unsigned char* p, u64& w0, u64& w1) {
+    const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+    const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
+    ws_hdr_from32(q[0], q[1], (u32)(pa & 15), w0, w1);
+}
+
+// header bytes [p, p + 16) (wave-uniform p) by scalar loads: S1 never changes header bytes
+__device__ __forceinline__ void spec_words_s(uintptr_t p, u64& w0, u64& w1) {
+    const HdrWords hw = load_header(reinterpret_cast<const unsigned char*>(p));
     const u64 lo = (u64)hw.w0 | ((u64)hw.w1 << 32), mi = (u64)hw.w2 | ((u64)hw.w3 << 32), hi = (u64)hw.w4;
     const u32 sh = 8u * (u32)(p & 3);
-    return ws_parse(sh ? (lo >> sh) | (mi << (64 - sh)) : lo, sh ? (mi >> sh) | (hi << (64 - sh)) : mi, avail);
+    w0 = sh ? (lo >> sh) | (mi << (64 - sh)) : lo;
+    w1 = sh ? (mi >> sh) | (hi << (64 - sh)) : mi;
 }
 
 __device__ __forceinline__ void spec_flag(u32* flags, u32* list, u32* head, u32 s) {
@@ -160,13 +192,44 @@ __device__ __forceinline__ void spec_flag(u32* flags, u32* list, u32* head, u32 
     }
 }
 
-template <int NT>
+// descriptor of a matched frame (the out-params websocketframeDecode gives it)
+__device__ __forceinline__ void spec_store_desc(WebsocketFrameDesc_t* d, u64 pos, u32 b0, u32 hdr, u32 masked, u32 g) {
+    const u64 plen = g - hdr;
+    const u64 dof = plen ? pos + hdr : WEBSOCKET_DATA_OFF_NULL;
+    u32x4 q0, q1;
+    q0.x = (u32)pos; q0.y = (u32)(pos >> 32); q0.z = (u32)dof; q0.w = (u32)(dof >> 32);
+    q1.x = (u32)plen; q1.y = 0; q1.z = g;
+    q1.w = (b0 >> 7) | ((b0 & 0x0Fu) << 8) | (masked << 16) | (hdr << 24);
+    gu32x4* gd = gptr<u32x4>(d);
+    gd[0] = q0;
+    gd[1] = q1;
+}
+
+// XOR frame payload bytes [a, b) of this wave's range (range-relative, clamped to [-16, RW + 16],
+// uniform) with `key` (rotated to the 16-B chunk phase): rows wholly inside take four XORs, only
+// edge rows work out per-lane byte bounds. cov: the payload bytes of each lane's chunk.
+__device__ __forceinline__ void spec_xor_rows(u32x4 (&v)[SPEC_U], u32 (&cov)[SPEC_U], int a, int b, u32 key, int xl) {
+#pragma unroll
+    for (int u = 0; u < SPEC_U; ++u) {
+        if (b <= u * 1024 || a >= u * 1024 + 1024) continue;                // (uniform) not in row u
+        if (a <= u * 1024 && b >= u * 1024 + 1024) {                        // (uniform) the whole row
+            v[u].x ^= key; v[u].y ^= key; v[u].z ^= key; v[u].w ^= key;
+            cov[u] = 0xFFFFu;
+            continue;
+        }
+        const int xx = u * 1024 + xl;
+        const int l2 = a > xx ? a - xx : 0, h2 = b < xx + 16 ? b - xx : 16;
+        if (h2 > l2) ws_xor_range(key, l2, h2, v[u], cov[u]);
+    }
+}
+
+template <int NT, int DBG>
 __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
     WebsocketSegResult_t* __restrict__ res, u32* head, u32* done, u32* flags, u32* list, u32* marks, u32 tag,
     u64 pbase, u64 c_lo, u64 c_hi, u64 lo, u64 hi, u64 ppw, u64 npieces, u32 wshift, u32 nchk, u32 chk_per,
-    u32 spins, u32 g32, float rg) {
+    u32 spins, SpecSig S) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u32 bx = blockIdx.x;
@@ -176,18 +239,25 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 wc0 = ((pbase + pidx) << (SPEC_SHIFT - 4)) + (u64)wv * (64 * SPEC_U);
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
-    // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
+    // the wave's 256 chunks lie inside the batch's chunks [c_lo, c_hi): no per-lane clamps
+    const bool inside = wc0 >= c_lo && wc0 + 64 * SPEC_U <= c_hi;
+    gu32x4* const wbase = base + wc0;
+    // ---- 1. payload loads (unconditional, clamped to the batch's chunks)
     u32x4 v[SPEC_U];
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) {
-        const u64 c = wc0 + (u64)(u * 64 + lane);
-        v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
+        if (inside) {
+            v[u] = ld16<NT>(wbase + (u * 64 + lane));
+        } else {
+            const u64 c = wc0 + (u64)(u * 64 + lane);
+            v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
+        }
     }
     const u32 gw = bx * (SPEC_T / 64) + wv;
     u32* const myrepl = done + (gw % SPEC_REPL) * (SPEC_REPL_STRIDE / 4);
     // the checkers' verdict, polled now so the load is back by the stores (a wave that finds
     // it not published yet polls again there)
-    u32 verdict = lane == 0 ? ld_agent(myrepl) : 0u;
+    u32 verdict = DBG == 4 ? 1u : (lane == 0 ? ld_agent(myrepl) : 0u);
     // ---- 2. checker duty (the first nchk waves): the segment table is ascending and inside
     //         [lo, hi) (the piece decomposition assumes it); zero-length results written here
     if (gw < nchk) {
@@ -220,10 +290,11 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     const u64 r0 = wc0 << 4, r1 = r0 + RW;                                  // origin-relative
     const u64 ra = r0 > lead0 ? r0 - lead0 : 0, rb = r1 - lead0;            // buffer-relative
     const int xl = (int)lane * 16;
-    const u64 g = g32;
+    const u64 g = S.g;
     u32 cov[SPEC_U], segcov[SPEC_U];
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) { cov[u] = 0; segcov[u] = 0; }
+    bool allseg = false;                                                    // one segment covers the range
     u32 s_first = 0, s_stop = 0;                                            // segments visited [s_first, s_stop)
     if (pvalid) {
         // ---- 3. the segments under [ra, rb): the last one starting at or before ra, then on
@@ -250,17 +321,18 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                 const u32 cc = lane == 0 ? ld_agent(myrepl) : 0u;           // stop walking garbage early
                 if (__builtin_amdgcn_readfirstlane(cc) == 2) break;
             }
-            s = uni32(s);
-            const u64 so = uni64(sld64(seg_off + s)), sl = uni64(sld64(seg_len + s));
+            const u64 so = sld64(seg_off + s), sl = sld64(seg_len + s);
             if (so >= rb) break;
             if (sl == 0 || (so < ra && sl <= ra - so)) continue;           // empty, or ends before the range
             if (so > hi || sl > hi - so) {                                  // outside the batch: the checkers
                 if (lane == 0) spec_flag(flags, list, head, s);             // mark it unordered, nothing is
                 continue;                                                   // stored; never load past it
             }
-            const u64 sorg = so + lead0;
-            {   // byte coverage by segments: chunks wholly inside segments are stored whole
-                const long long sa = (long long)(sorg - r0), sbb = sa + (long long)sl;
+            // segment start relative to the range (origin coordinates: so + lead0 - r0)
+            const long long sa = (long long)(so + lead0) - (long long)r0, sbb = sa + (long long)sl;
+            if (sa <= 0 && sbb >= RW) {
+                allseg = true;                                              // chunks all inside: stored whole
+            } else {
                 const int SA = (int)(sa < -16 ? -16 : (sa > RW + 16 ? RW + 16 : sa));
                 const int SB = (int)(sbb < -16 ? -16 : (sbb > RW + 16 ? RW + 16 : sbb));
 #pragma unroll
@@ -271,48 +343,46 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                     if (h2 > l2) segcov[u] |= (0xFFFFu >> (16 - h2)) & (0xFFFFu << l2);
                 }
             }
-            const SpecPred pr = spec_predict(sl, g, rg, max_frames);
+            // frames predicted: nfull = min(sl / g, max_frames)
+            const u64 q = spec_div(sl, g, S.rg);
+            const u32 nfull = q < max_frames ? (u32)q : max_frames;
+            if (sa >= 0 && sa < RW && lane == 0)                            // the wave holding byte 0: result
+                ws_store_res(res + s, (u64)nfull * g, nfull,
+                             nfull == max_frames && (u64)nfull * g < sl ? WEBSOCKET_SEG_MAX_FRAMES : WEBSOCKET_SEG_OK);
+            // frames k = kA.. whose start lies in front of r1 (kA: the frame holding r0); their
+            // range-relative starts fr in 32 bits (g < 2^30: fr in (-g, RW + g))
+            u32 kA = 0;
+            int fr = (int)sa;
+            if (sa < 0) {
+                const u64 qa = spec_div((u64)(-sa), g, S.rg);
+                kA = (u32)qa;
+                fr = (int)(sa + (long long)(qa * g));
+            }
+            const u64 dbase = desc_base ? sld64(desc_base + s) : (u64)s * max_frames;
             bool bad = false;
-            if (lane == 0 && sorg >= r0 && sorg < r1)                       // result: the wave holding byte 0
-                ws_store_res(res + s, (u64)pr.n * g, pr.n, pr.status);
-            const u64 kend = (u64)pr.n + (pr.tail ? 1u : 0u);               // + the tail header to check
-            const u64 kA = uni64(r0 > sorg ? spec_div(r0 - sorg, g, rg) : 0);    // frame holding r0
-            u64 kB = spec_div(r1 - sorg + g - 1, g, rg);                    // frames starting before r1
-            kB = uni64(kB > kend ? kend : kB);
-            const u64 dbase = uni64(desc_base ? sld64(desc_base + s) : (u64)s * max_frames);
-            // one scalar header load per frame, the next one issued before the current one is
-            // parsed (1-2 frames per 4 KiB range at cfg2's frames)
-            const u32 nfr = uni32(kB > kA ? (u32)(kB - kA) : 0u);
-            HdrWords hn = load_header(buf + uni64(so + kA * g));
-            for (u32 i = 0; i < nfr; ++i) {
-                const u64 k = uni64(kA + i);
-                const u64 pos = uni64(so + k * g);
-                const HdrWords hc = hn;
-                if (i + 1 < nfr) hn = load_header(buf + uni64(pos + g));
-                const WsHdr h = spec_parse_words(hc, reinterpret_cast<uintptr_t>(buf) + pos, sl - k * g);
-                const u64 porg = pos + lead0;
-                const bool tail = pr.tail && k == pr.n;
-                if (porg >= r0 && porg < r1) {                              // this wave owns the header
-                    if (tail) bad |= h.kind != WS_PARSE_INCOMPLETE;
-                    else if (h.kind == WS_PARSE_FRAME && (u64)h.hdr + h.plen == g) {
-                        if (lane == 0) ws_store_desc(desc + dbase + k, pos, h);
-                    } else bad = true;
+            for (u32 k = kA; DBG != 1 && fr < (int)RW; ++k, fr += (int)g) {
+                const u64 rel = (u64)k * g, pos = so + rel;                 // segment- / buffer-relative
+                u64 w0, w1;
+                if (k >= nfull) {                                           // past the predicted frames: the
+                    if (k == nfull && k < max_frames && fr >= 0 && sl - rel >= 2) {   // tail must stay incomplete
+                        spec_words_s(reinterpret_cast<uintptr_t>(buf) + pos, w0, w1);
+                        bad |= ws_parse(w0, w1, sl - rel).kind != WS_PARSE_INCOMPLETE;
+                    }
+                    break;
                 }
-                if (tail || h.kind != WS_PARSE_FRAME || !h.masked || h.hdr >= g) continue;   // the XOR rule
-                const u64 p0 = porg + h.hdr, p1 = porg + g;
-                if (p1 <= r0 || p0 >= r1) continue;
-                const long long qa = (long long)(p0 - r0), qb = (long long)(p1 - r0);
-                const int a = (int)(qa < -16 ? -16 : (qa > RW + 16 ? RW + 16 : qa));
-                const int bb = (int)(qb < -16 ? -16 : (qb > RW + 16 ? RW + 16 : qb));
-                const u32 key = rotl32(h.key, 8u * (u32)(p0 & 3));
-#pragma unroll
-                for (int u = 0; u < SPEC_U; ++u) {
-                    if (bb <= u * 1024 || a >= u * 1024 + 1024) continue;       // (uniform) not in row u
-                    const int xx = u * 1024 + xl;
-                    const int l2 = a > xx ? a - xx : 0, h2 = bb < xx + 16 ? bb - xx : 16;
-                    if (h2 <= l2) continue;
-                    ws_xor_range(key, l2, h2, v[u], cov[u]);
+                spec_words_s(reinterpret_cast<uintptr_t>(buf) + pos, w0, w1);
+                u32 hdr, masked, key;
+                const bool ok = spec_match(w0, w1, S, hdr, masked, key);
+                if (fr >= 0) {                                              // this wave owns the header
+                    if (!ok) bad = true;
+                    else if (lane == 0 && DBG != 3) spec_store_desc(desc + dbase + k, pos, (u32)w0 & 0xFFu, hdr, masked, (u32)g);
                 }
+                if (!ok || !masked || DBG == 2) continue;                   // the XOR rule
+                const int qa = fr + (int)hdr, qb = fr + (int)g;
+                if (qb <= 0 || qa >= (int)RW) continue;
+                // (origin-relative payload start r0 + qa: the key rotated to the chunk phase)
+                spec_xor_rows(v, cov, qa < -16 ? -16 : qa, qb > (int)RW + 16 ? (int)RW + 16 : qb,
+                              rotl32(key, 8u * (((u32)r0 + (u32)qa) & 3u)), xl);
             }
             if (bad && lane == 0) spec_flag(flags, list, head, s);
         }
@@ -343,10 +413,10 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) {
         const u64 cidx = wc0 + (u64)(u * 64 + lane);
-        if (!cov[u] || cidx < c_lo || cidx >= c_hi) continue;
-        const u32x4 w = v[u];
-        if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) st16<NT>(w, base + cidx);
-        else ws_store_bytes(reinterpret_cast<gu8*>(base + cidx), w, cov[u]);
+        if (!cov[u] || (!inside && (cidx < c_lo || cidx >= c_hi))) continue;
+        gu32x4* const pc = wbase + (u * 64 + lane);
+        if (cov[u] == 0xFFFFu || allseg || segcov[u] == 0xFFFFu) st16<NT>(v[u], pc);
+        else ws_store_bytes(reinterpret_cast<gu8*>(pc), v[u], cov[u]);
     }
 }
 
@@ -395,7 +465,9 @@ __device__ __forceinline__ void spec_walk(unsigned char* __restrict__ buf, u32 s
         if (nf >= max_frames) { status = WEBSOCKET_SEG_MAX_FRAMES; break; }
         if (sl - off < 2) break;                                        // websocketframe.c:121
         unsigned char* const p = seg + off;
-        const WsHdr h = spec_header(p, sl - off);
+        u64 w0, w1;
+        spec_words_v(p, w0, w1);
+        const WsHdr h = ws_parse(w0, w1, sl - off);
         if (h.kind == WS_PARSE_INCOMPLETE) break;
         if (h.kind == WS_PARSE_WRAP) { status = WEBSOCKET_SEG_ERR_LEN_WRAP; break; }
         if (h.masked) unmask_payload<4, NT>(p + h.hdr, p + h.hdr + h.plen, h.key, lane);
@@ -413,14 +485,14 @@ __global__ __launch_bounds__(256) void ws_piece_spec_fix_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
     WebsocketSegResult_t* __restrict__ res, const u32* head, u32* next_head, u32* next_done, u32* flags,
-    const u32* list, const u32* marks, u32 tag, u64 pbase, u32 g32, float rg, int* advice) {
+    const u32* list, const u32* marks, u32 tag, u64 pbase, SpecSig S, int* advice) {
     const u32 lane = threadIdx.x & 63;
     const u32 gw = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const u32 nw = gridDim.x * 4;
     const u32 c = *gptr<u32>(head + SPEC_CTR), nmis = *gptr<u32>(head + SPEC_NMIS);
     const bool tmo = *gptr<u32>(head + SPEC_TMO) != 0;
     const u64 rbase = pbase << (SPEC_SHIFT - SPEC_RANGE_SHIFT);
-    const u64 g = g32;
+    const u64 g = S.g;
     if (c >> 16) {
         // unordered (or outside [lo, hi)): S1 stored nothing; the reactor loop per segment
         for (u32 s = gw; s < nseg; s += nw) spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
@@ -429,12 +501,14 @@ __global__ __launch_bounds__(256) void ws_piece_spec_fix_kernel(
         for (u32 i = gw; i < nmis; i += nw) {
             const u32 s = list[i];
             const u64 so = seg_off[s], sl = seg_len[s];
-            const SpecPred pr = spec_predict(sl, g, rg, max_frames);
-            for (u32 k = 0; k < pr.n; ++k) {                           // undo S1's XOR where it stored
-                unsigned char* const p = buf + so + (u64)k * g;
-                const WsHdr h = spec_header(p, sl - (u64)k * g);
-                if (h.kind == WS_PARSE_FRAME && h.masked && h.hdr < g)
-                    spec_xor_stored<NT>(buf, p + h.hdr, p + g, h.key, marks, tag, rbase, tmo, lane);
+            // undo S1's XOR where it stored: the same rule over the same (unchanged) header bytes
+            for (u64 k = 0; k < max_frames && (k + 1) * g <= sl; ++k) {
+                unsigned char* const p = buf + so + k * g;
+                u64 w0, w1;
+                spec_words_v(p, w0, w1);
+                u32 hdr, masked, key;
+                if (spec_match(w0, w1, S, hdr, masked, key) && masked)
+                    spec_xor_stored<NT>(buf, p + hdr, p + g, key, marks, tag, rbase, tmo, lane);
             }
             spec_walk<NT>(buf, s, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
             if (lane == 0) *gptr<u32>(flags + s) = 0;
@@ -487,13 +561,13 @@ bool ws_spec_fits(u64 span, u32 nseg) {
     return npieces >= 1 && nseg >= 1 && (u64)nseg <= nchk * 256;
 }
 
-// g: the frame wire length to predict every segment with (>= 2)
+// g: the frame wire length to predict every segment with (2 <= g < 2^30)
 int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, u32 g,
                          int* advice_dev) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     const u64 npieces = hi_org > lo_org ? ((hi_org - 1) >> SPEC_SHIFT) - (lo_org >> SPEC_SHIFT) + 1 : 0;
-    if (!npieces || g < 2 || g >= (1u << 31)) return ws_set_msg("spec decode: empty range or no frame length");
+    if (!npieces || g < 2 || g >= (1u << 30)) return ws_set_msg("spec decode: empty range or frame length out of range");
     const u64 pbase = lo_org >> SPEC_SHIFT, c_lo = lo_org >> 4, c_hi = (hi_org + 15) >> 4;
     const u32 p = parity & 1;
     u32* head = reinterpret_cast<u32*>(sws) + SPEC_HEAD_WORDS * p;
@@ -512,22 +586,25 @@ int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, 
     const u32 nchk = (u32)(waves < 1024 ? waves : 1024);
     const u32 chk_per = (u32)((L.nseg + nchk - 1) / nchk);
     if (chk_per > 256) return ws_set_msg("spec decode: too many segments for the checkers");
-    const float rg = 1.0f / (float)g;
+    const SpecSig S = spec_sig(g);
     size_t tslot = 0;
     int rc;
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    hipLaunchKernelGGL(ws_piece_spec_kernel<1>, dim3((u32)grid), dim3(SPEC_T), ws_piece_dyn_lds(L), L.stream, L.buf,
+    const int dbg = ws_spec_dbg;
+    auto kern = dbg == 1 ? ws_piece_spec_kernel<1, 1> : dbg == 2 ? ws_piece_spec_kernel<1, 2> : dbg == 3 ? ws_piece_spec_kernel<1, 3>
+              : dbg == 4 ? ws_piece_spec_kernel<1, 4> : ws_piece_spec_kernel<1, 0>;
+    hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(SPEC_T), ws_piece_dyn_lds(L), L.stream, L.buf,
                        L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, done, flags, list,
                        marks, tag, pbase, c_lo, c_hi, lo, hi, ppw, npieces, wshift, nchk, chk_per,
-                       (u32)(int)ws_spec_spins, g, rg);
+                       (u32)(int)ws_spec_spins, S);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_spec_kernel launch", e);
     if (timing && (rc = ws_k2_mark(L.stream, true, &tslot))) return rc;
     const u32 fix_blocks = (u32)((L.nseg + 3) / 4 < 256 ? (L.nseg + 3) / 4 : 256);
     hipLaunchKernelGGL(ws_piece_spec_fix_kernel<1>, dim3(fix_blocks), dim3(256), 0, L.stream, L.buf, L.seg_off,
                        L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, next_head, next_done, flags,
-                       list, marks, tag, pbase, g, rg, advice_dev);
+                       list, marks, tag, pbase, S, advice_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_spec_fix_kernel launch", e);
     return 0;
