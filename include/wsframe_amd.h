@@ -212,7 +212,9 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * (path 3: 0 always the scan kernel + unmask, 1 adaptive — speculative, with no scan kernel,
  * when the previous eager call on the stream advised it — 2 speculative whenever the batch
  * fits), "spec_spins" (the speculative kernel's bounded wait for its table checkers; 0 gives
- * up at once, exercising its repair path), "piece_lds" (unused dynamic LDS per unmask block:
+ * up at once, exercising its repair path), "spec_g" (0: the speculative kernel predicts
+ * frames of the length the previous call on the stream saw first; >= 2 forces that length,
+ * for tests of mispredictions), "piece_lds" (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 5), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the

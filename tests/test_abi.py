@@ -242,7 +242,7 @@ import sys
 sys.path.insert(0, sys.argv[1])
 from util_amd import wsframe as W
 names = sys.argv[2].split(",")
-VAL = {"stream_rw_cmax": 20}                                # (16..26)
+VAL = {"stream_rw_cmax": 20, "spec_g": 0}                 # (16..26; 0 or >= 2)
 bad = [n for n in names if W.load_lib().websocketframeGpuSetOption(n.encode(), VAL.get(n, 1)) != 0]
 unknown_ok = W.load_lib().websocketframeGpuSetOption(b"no_such_option", 1) == 0
 print("BAD", bad, "UNKNOWN_ACCEPTED", unknown_ok)

@@ -105,50 +105,56 @@ def anomalous(rng, kind, plen):
     return frame(rng, 0)
 
 
+@pytest.mark.parametrize("gap", [True, False], ids=["gaps", "contiguous"])
 @pytest.mark.parametrize("kind", ANOMALIES)
-@pytest.mark.parametrize("plen", [1000, 100, 4096])
-def test_misprediction_at_every_frame_index(dev, kind, plen):
+@pytest.mark.parametrize("plen", [1000, 100, 4096, 2500, 70000])
+def test_misprediction_at_every_frame_index(dev, kind, plen, gap):
     """16-frame segments of equal frames, segment j broken at frame 1 + j % 15 (every index
-    1..15, several times), next to unbroken segments: every broken segment is repaired"""
-    rng = np.random.default_rng(ANOMALIES.index(kind) * 10007 + plen)
+    1..15, several times), next to unbroken segments: every broken segment is repaired.
+    Frames of >= 2 KiB take S1's fast path (its frames in scalar registers), across a
+    segment boundary too when the segments are contiguous; 70000 B: the 64-bit length form"""
+    rng = np.random.default_rng(ANOMALIES.index(kind) * 10007 + plen + gap)
     segs = []
-    for j in range(96):
+    for j in range(96 if plen < 10000 else 30):
         parts = [frame(rng, plen) for _ in range(16)]
         if j % 3 != 2:
             parts[1 + j % 15] = anomalous(rng, kind, plen)
         segs.append(parts)
-    wire, so, sl = batch(segs, rng)
+    wire, so, sl = batch(segs, rng, gap=gap)
     check(dev, wire, so, sl, 16, "%s plen %d" % (kind, plen), wirelen(plen))
     check(dev, wire, so, sl, 20, "%s plen %d max 20" % (kind, plen), wirelen(plen))
 
 
+@pytest.mark.parametrize("plen", [700, 4096])
 @pytest.mark.parametrize("tail", ["exact", "hdr1", "hdr5", "payload_short", "shorter_complete", "garbage",
                                   "longer_incomplete", "zero_frame"])
-def test_segment_tails(dev, tail):
+def test_segment_tails(dev, tail, plen):
     """what follows the last predicted frame: nothing, an incomplete header or payload (the
-    reference stops, consumed excludes it), a complete shorter frame (misprediction), garbage"""
-    rng = np.random.default_rng(5)
+    reference stops, consumed excludes it), a complete shorter frame (misprediction), garbage;
+    segments back to back (4096: S1's fast path reaches the tails' ranges)"""
+    rng = np.random.default_rng(5 + plen)
     segs = []
     for j in range(80):
         n = 1 + j % 16
-        parts = [frame(rng, 700) for _ in range(n)]
-        extra = {"exact": b"", "hdr1": b"\x82", "hdr5": frame(rng, 700)[:5],
-                 "payload_short": frame(rng, 700)[:500], "shorter_complete": frame(rng, 10),
+        parts = [frame(rng, plen) for _ in range(n)]
+        extra = {"exact": b"", "hdr1": b"\x82", "hdr5": frame(rng, plen)[:5],
+                 "payload_short": frame(rng, plen)[:plen - 200], "shorter_complete": frame(rng, 10),
                  "garbage": rng.integers(0, 256, 300, dtype=np.uint8).tobytes(),
-                 "longer_incomplete": frame(rng, 5000)[:650], "zero_frame": frame(rng, 0)}[tail]
+                 "longer_incomplete": frame(rng, plen * 7)[:plen - 50], "zero_frame": frame(rng, 0)}[tail]
         segs.append(parts + [extra])
-    wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, 17, tail, wirelen(700))
+    wire, so, sl = batch(segs, rng, gap=plen == 700)
+    check(dev, wire, so, sl, 17, tail, wirelen(plen))
 
 
+@pytest.mark.parametrize("plen", [300, 3000])
 @pytest.mark.parametrize("max_frames", [1, 2, 7, 16, 64])
-def test_max_frames(dev, max_frames):
+def test_max_frames(dev, max_frames, plen):
     """segments of 16 equal frames (+ a partial one) under every descriptor capacity:
-    MAX_FRAMES predicted exactly when frames remain"""
-    rng = np.random.default_rng(max_frames)
-    segs = [[frame(rng, 300) for _ in range(16)] + ([frame(rng, 300)[:100]] if j % 2 else []) for j in range(64)]
-    wire, so, sl = batch(segs, rng)
-    check(dev, wire, so, sl, max_frames, "max_frames %d" % max_frames, wirelen(300))
+    MAX_FRAMES predicted exactly when frames remain (3000: the fast path, contiguous segments)"""
+    rng = np.random.default_rng(max_frames + plen)
+    segs = [[frame(rng, plen) for _ in range(16)] + ([frame(rng, plen)[:100]] if j % 2 else []) for j in range(64)]
+    wire, so, sl = batch(segs, rng, gap=plen == 300)
+    check(dev, wire, so, sl, max_frames, "max_frames %d" % max_frames, wirelen(plen))
 
 
 def test_first_frame_quirks(dev):
@@ -265,16 +271,18 @@ def test_state_across_calls_and_shapes(dev):
 
 def test_adaptive_choice(dev):
     """piece_spec 1 (the default): the first call on a stream takes the scan kernel, which
-    advises the speculative path for a batch of equal frames; a batch of mixed lengths makes
-    the repair kernel advise the scan kernel again. Every call bit-exact."""
+    advises the speculative path for a batch of equal frames of >= 48 KiB; a batch of mixed
+    lengths makes the repair kernel advise the scan kernel again; equal frames below 48 KiB
+    stay on the scan kernel (profiles/r03_spec_sweep.log). Every call bit-exact."""
     W.set_option("piece_spec", 1)
     W.set_option("spec_g", 0)
     rng = np.random.default_rng(60)
     stream = torch.cuda.Stream(dev)
-    uni = batch([[frame(rng, 2000) for _ in range(16)] for _ in range(200)], rng)
+    uni = batch([[frame(rng, 50000) for _ in range(4)] for _ in range(40)], rng)
+    small = batch([[frame(rng, 2000) for _ in range(16)] for _ in range(200)], rng)
     mixed = P.random_stream(np.random.default_rng(61), 600)
     seq = [(uni, False), (uni, True), (uni, True), (mixed, True), (mixed, False), (mixed, False), (uni, False),
-           (uni, True)]
+           (uni, True), (small, True), (small, False), (small, False), (uni, False), (uni, True)]
     with torch.cuda.stream(stream):
         for k, ((wire, so, sl), want_spec) in enumerate(seq):
             n0 = spec_calls()

@@ -30,7 +30,7 @@ extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
-extern WsOpt ws_spec_spins, ws_spec_dbg;
+extern WsOpt ws_spec_spins;
 WsOpt ws_spec_g{0};        // "spec_g": the frame length the speculative path predicts with (0: the device's hint)
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
@@ -55,6 +55,7 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 
 static WsOpt g_path{-1};   // "path": -1 auto (4 for many small segments, else 3), 1 walker (one wave per
                            // segment), 3 piece (K1 + K2, or the speculative S1 + S2), 4 segfuse
+#define WS_SPEC_ADAPT_G 49152
 WsOpt ws_piece_spec{1};    // "piece_spec": 0 never speculative, 1 adaptive (the device's advice from the
                            // previous call on the slot), 2 speculative whenever the batch fits
 
@@ -107,7 +108,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
     }
-    else if (!strcmp(name, "spec_dbg")) ws_spec_dbg = (int)value;
     else if (!strcmp(name, "spec_g")) {
         if (value < 0 || value >= (1ll << 31) || value == 1) return -1;
         ws_spec_g = (int)value;
@@ -544,12 +544,15 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         const int spec_opt = ws_piece_spec;
         if (!cap && (rc = slot.advice(&adv_h, &adv_d))) return rc;
         // speculative (no K1): eager calls only, when the checkers can cover the segment table,
-        // and when the device advised it after the previous call on this slot (or forced)
+        // and, adaptive, when the device advised it after the previous call on this slot and
+        // that call's first frame was >= WS_SPEC_ADAPT_G bytes (below that the classic form is
+        // as fast or faster: K1 costs little there, and K2 right behind K1 streams faster than
+        // any one-pass kernel, profiles/r03_spec_sweep.log); forced: whenever it fits
         // (the device's advice and frame-length hint: adv_h[0], adv_h[1]; option spec_g overrides the hint)
         int hint = ws_spec_g > 0 ? (int)ws_spec_g : __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED);
         if (spec_opt == 2 && hint < 2) hint = 1024;     // forced with no hint yet: any length verifies
         if (!cap && spec_opt && hint >= 2 && hint < (1 << 30) && ws_spec_fits(hi - lo, nseg) &&
-            (spec_opt == 2 || __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1)) {
+            (spec_opt == 2 || (__atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1 && hint >= WS_SPEC_ADAPT_G))) {
             unsigned char* sws = nullptr;
             u32 parity = 0, tag = 0;
             if ((rc = slot.spec(hi - lo, nseg, &sws, &parity, &tag))) return rc;

@@ -45,12 +45,12 @@
 #define SPEC_T 256
 #define SPEC_U WS_PIECE_U
 #define SPEC_SHIFT WS_PIECE_SHIFT
+#define SPEC_FAST_G 2048                    // fast path: at most 3 frames touch a wave's range
 #define SPEC_RANGE_SHIFT 12                 // one wave's range: 64 lanes x SPEC_U x 16 B = 4 KiB
 static_assert((1 << SPEC_RANGE_SHIFT) == 64 * SPEC_U * 16, "wave range");
 // bounded wait for the checkers (s_sleep 2 + a load each): option "spec_spins" (0 = give up
 // unless the first poll finds them done: exercises the repair path in tests)
 WsOpt ws_spec_spins{2048};
-WsOpt ws_spec_dbg{0};     // TEMPORARY: instruction-count experiments
 
 enum { SPEC_CTR = 0, SPEC_NMIS = 1, SPEC_TMO = 2, SPEC_HEAD_WORDS = 4 };
 // the checkers' verdict, published by the last checker into SPEC_REPL words SPEC_REPL_STRIDE
@@ -67,7 +67,12 @@ struct SpecSig {
     u32 e16[2];       // 16-bit form: bytes 2-3 read little-endian (0x10000: impossible)
     u32 ok64[2];      // the 64-bit form is possible (g >= 10 + 4m)
     float rg;         // 1.0f / g
+    float gs;         // segments per 256 bytes of the batch (the table guess)
     u64 e64[2];       // 64-bit form: bytes 2-9 read little-endian
+    // g >= SPEC_FAST_G: the masked frame in its shortest form (16- or 64-bit length) as masked
+    // compares of the header's first three dwords; the key at dword 1 (16-bit) or bytes 10-13
+    u32 fm[3], fe[3];
+    u32 f64, fhdr;
 };
 
 static SpecSig spec_sig(u32 g) {
@@ -80,6 +85,21 @@ static SpecSig spec_sig(u32 g) {
         S.e16[m] = g >= h16 && g - h16 <= 0xFFFF ? (((g - h16) >> 8) | (((g - h16) & 0xFFu) << 8)) : 0x10000u;
         S.ok64[m] = g >= h64;
         S.e64[m] = g >= h64 ? __builtin_bswap64((u64)(g - h64)) : 0;
+    }
+    S.f64 = g - 8 > 0xFFFFu;
+    S.fhdr = S.f64 ? 14 : 8;
+    const u64 len = g - S.fhdr;
+    S.fm[0] = 0xFFFFFF00u;
+    if (!S.f64) {
+        S.fe[0] = 0xFE00u | (u32)((len >> 8) & 0xFF) << 16 | (u32)(len & 0xFF) << 24;
+        S.fm[1] = S.fe[1] = S.fm[2] = S.fe[2] = 0;
+    } else {
+        const u64 be = __builtin_bswap64(len);          // bytes 2-9 in wire order
+        S.fe[0] = 0xFF00u | (u32)(be & 0xFFFF) << 16;
+        S.fm[1] = 0xFFFFFFFFu;
+        S.fe[1] = (u32)(be >> 16);
+        S.fm[2] = 0xFFFFu;
+        S.fe[2] = (u32)(be >> 48);
     }
     return S;
 }
@@ -223,7 +243,7 @@ __device__ __forceinline__ void spec_xor_rows(u32x4 (&v)[SPEC_U], u32 (&cov)[SPE
     }
 }
 
-template <int NT, int DBG>
+template <int NT>
 __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     unsigned char* __restrict__ buf, const u64* __restrict__ seg_off, const u64* __restrict__ seg_len, u32 nseg,
     u32 max_frames, const u64* __restrict__ desc_base, WebsocketFrameDesc_t* __restrict__ desc,
@@ -238,27 +258,43 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     const bool pvalid = pw < npieces;
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 wc0 = ((pbase + pidx) << (SPEC_SHIFT - 4)) + (u64)wv * (64 * SPEC_U);
-    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
-    // the wave's 256 chunks lie inside the batch's chunks [c_lo, c_hi): no per-lane clamps
-    const bool inside = wc0 >= c_lo && wc0 + 64 * SPEC_U <= c_hi;
-    gu32x4* const wbase = base + wc0;
-    // ---- 1. payload loads (unconditional, clamped to the batch's chunks)
+    // ---- 1. payload loads: chunk rel = u * 64 + lane of the wave's 256, clamped into the batch's
+    //         chunks [c_lo, c_hi) as med3(rel, A, B) (A <= B; only a batch's edge waves clamp)
+    int A, B;
+    {
+        const long long dlo = (long long)(c_lo - wc0), dhi = (long long)(c_hi - 1 - wc0);
+        const long long a0 = dhi < 0 ? dhi : 0, b0 = dlo > 255 ? dlo : 255;
+        A = (int)(dlo > a0 ? dlo : a0);
+        B = (int)(dhi < b0 ? dhi : b0);
+    }
+    const uintptr_t sbase = (reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15) + (wc0 << 4) + (uintptr_t)(long long)A * 16;
     u32x4 v[SPEC_U];
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) {
-        if (inside) {
-            v[u] = ld16<NT>(wbase + (u * 64 + lane));
-        } else {
-            const u64 c = wc0 + (u64)(u * 64 + lane);
-            v[u] = ld16<NT>(base + (c < c_lo ? c_lo : (c < c_hi ? c : c_hi - 1)));
-        }
+        const int rel = u * 64 + (int)lane;
+        const int rc = rel < A ? A : (rel > B ? B : rel);
+        v[u] = ld16<NT>(reinterpret_cast<gu32x4*>(sbase + (u32)((rc - A) * 16)));
     }
     const u32 gw = bx * (SPEC_T / 64) + wv;
     u32* const myrepl = done + (gw % SPEC_REPL) * (SPEC_REPL_STRIDE / 4);
     // the checkers' verdict, polled now so the load is back by the stores (a wave that finds
     // it not published yet polls again there)
-    u32 verdict = DBG == 4 ? 1u : (lane == 0 ? ld_agent(myrepl) : 0u);
-    // ---- 2. checker duty (the first nchk waves): the segment table is ascending and inside
+    u32 verdict = lane == 0 ? ld_agent(myrepl) : 0u;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    constexpr long long RW = 64 * SPEC_U * 16;                              // this wave's bytes
+    const u64 r0 = wc0 << 4, r1 = r0 + RW;                                  // origin-relative
+    const u64 ra = r0 > lead0 ? r0 - lead0 : 0, rb = r1 - lead0;            // buffer-relative
+    // ---- 2. the segment holding ra: a guess from the batch's extent (kernel arguments), checked
+    //         by the four table entries of it and its successor, loaded at once
+    u32 guess = 0;
+    if (nseg > 2 && ra > lo) {
+        const float f = (float)(u32)((ra - lo) >> 8) * S.gs;
+        guess = uni32(f < (float)(nseg - 2) ? (u32)f : nseg - 2);
+    }
+    const u32 g1 = nseg > 1 ? guess + 1 : guess;
+    const u64 o0 = pvalid ? sld64(seg_off + guess) : 0, o1 = pvalid ? sld64(seg_off + g1) : 0;
+    const u64 l0 = pvalid ? sld64(seg_len + guess) : 0, l1 = pvalid ? sld64(seg_len + g1) : 0;
+    // ---- 3. checker duty (the first nchk waves): the segment table is ascending and inside
     //         [lo, hi) (the piece decomposition assumes it); zero-length results written here
     if (gw < nchk) {
         const u64 s_beg = (u64)gw * chk_per;
@@ -285,10 +321,6 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                                __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
-    constexpr long long RW = 64 * SPEC_U * 16;                              // this wave's bytes
-    const u64 r0 = wc0 << 4, r1 = r0 + RW;                                  // origin-relative
-    const u64 ra = r0 > lead0 ? r0 - lead0 : 0, rb = r1 - lead0;            // buffer-relative
     const int xl = (int)lane * 16;
     const u64 g = S.g;
     u32 cov[SPEC_U], segcov[SPEC_U];
@@ -297,26 +329,130 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     bool allseg = false;                                                    // one segment covers the range
     u32 s_first = 0, s_stop = 0;                                            // segments visited [s_first, s_stop)
     if (pvalid) {
-        // ---- 3. the segments under [ra, rb): the last one starting at or before ra, then on
-        const u64 first = sld64(seg_off), last_end = sld64(seg_off + nseg - 1) + sld64(seg_len + nseg - 1);
-        u32 guess = 0;
-        if (ra > first && last_end > first) {   // (f32 is exact enough: the guess is checked)
-            const float f = (float)(ra - first) * __builtin_amdgcn_rcpf((float)(last_end - first));
-            guess = f >= 1.0f ? nseg - 1 : (u32)(f * (float)nseg);
-            guess = uni32(guess < nseg ? guess : nseg - 1);
-        }
         u32 s;
-        {   // the guess, checked by two scalar loads (uniform segments: always right)
-            const u64 o0 = sld64(seg_off + guess), o1 = guess + 1 < nseg ? sld64(seg_off + guess + 1) : ~0ull;
-            if ((o0 <= ra && ra < o1) || (guess == 0 && ra < o0)) {
-                s = guess;
-            } else {
-                const u32 P = spec_count_le(seg_off, nseg, ra, guess, lane);
-                s = P ? P - 1 : 0;
-            }
+        bool hit = true;                         // s is guess or g1: its entries (and the next) are loaded
+        if (o0 <= ra && (ra < o1 || nseg == 1)) s = guess;
+        else if (guess == 0 && ra < o0) s = 0;
+        else if (nseg > 1 && o1 <= ra && g1 + 1 == nseg) { s = g1; hit = false; }
+        else {
+            const u32 P = spec_count_le(seg_off, nseg, ra, guess, lane);
+            s = P ? P - 1 : 0;
+            hit = false;
         }
         s_first = s;
-        for (u32 it = 1; s < nseg; ++s, ++it) {
+        bool fast = false;
+        if (g >= SPEC_FAST_G) {
+            // ---- 3a. fast path: one segment covers the range and every frame that touches it
+            //          is a predicted frame (the frames fit in scalar registers, each lane
+            //          picks its chunk's frame by two compares)
+            const u64 so = hit ? o0 : sld64(seg_off + s), sl = hit ? l0 : sld64(seg_len + s);
+            const long long sa = (long long)(so + lead0) - (long long)r0, send = sa + (long long)sl;
+            if (sa < 0 && sa > -(1ll << 31) && send > 0 && so <= hi && sl <= hi - so) {
+                const u32 x = (u32)(-sa), gg = (u32)g;
+                u32 kA = uni32((u32)((float)x * S.rg)), t = kA * gg;     // f32 estimate, off by <= 1
+                if (t > x) { --kA; t -= gg; }
+                else if (x - t >= gg) { ++kA; t += gg; }
+                const int F0 = (int)t - (int)x;                                    // (-g, 0]
+                const int nfr = 1 + (F0 + (int)gg < (int)RW) + (F0 + 2 * (int)gg < (int)RW);
+                const long long fend = (long long)F0 + (long long)nfr * gg;          // end of the last frame
+                u32 jb = 3, nfull2 = 0;                 // frames j >= jb belong to segment s + 1
+                u64 so2 = 0, sl2 = 0;
+                if (send >= RW) {                       // one segment covers the range
+                    fast = kA + (u32)nfr <= max_frames && fend <= send;
+                } else if (s + 1 < nseg) {
+                    // segment s ends inside the range on a frame boundary and s + 1 follows at once,
+                    // covering the rest: one train of frames (the wave holds s + 1's first byte)
+                    const u32 d = (u32)(send - F0);
+                    jb = (d >= gg) + (d >= 2 * gg);
+                    so2 = hit ? o1 : sld64(seg_off + s + 1);
+                    sl2 = hit ? l1 : sld64(seg_len + s + 1);
+                    if (d == jb * gg && kA + jb <= max_frames && (u32)nfr - jb <= max_frames && so2 == so + sl &&
+                        sl2 < (1ull << 31) && so2 <= hi && sl2 <= hi - so2 && fend <= send + (long long)sl2) {
+                        u32 q = uni32((u32)((float)(u32)sl2 * S.rg)), t2 = q * gg;
+                        if (t2 > (u32)sl2) --q;
+                        else if ((u32)sl2 - t2 >= gg) ++q;
+                        nfull2 = q < max_frames ? q : max_frames;
+                        fast = true;
+                    }
+                }
+                if (fast) {
+                    allseg = true;
+                    s_stop = jb < 3 ? s + 2 : s + 1;
+                    const u64 dbase = desc_base ? sld64(desc_base + s) : (u64)s * max_frames;
+                    const u64 dbase2 = jb == 3 ? 0 : (desc_base ? sld64(desc_base + s + 1) : (u64)(s + 1) * max_frames);
+                    if (jb < 3 && lane == 0)            // the predicted result of segment s + 1
+                        ws_store_res(res + s + 1, (u64)nfull2 * gg, nfull2,
+                                     nfull2 == max_frames && (u64)nfull2 * gg < sl2 ? WEBSOCKET_SEG_MAX_FRAMES
+                                                                                    : WEBSOCKET_SEG_OK);
+                    const u64 rpos = r0 - lead0;                                    // buffer offset of range byte 0
+                    int Fj[3], Pj[3];
+                    u32 RK[3];
+                    bool bad = false, bad2 = false;
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const int F = F0 + j * (int)gg;
+                        Fj[j] = F;
+                        Pj[j] = 0x40000000;
+                        RK[j] = 0;
+                        if (j && F >= (int)RW) continue;
+                        const u64 pos = rpos + (u64)(long long)F;
+                        const uintptr_t pa = reinterpret_cast<uintptr_t>(buf) + pos;
+                        const HdrWords hw = load_header(reinterpret_cast<const unsigned char*>(pa));
+                        const u32 sh = 8u * (u32)(pa & 3);
+                        const u32 d0 = (u32)((((u64)hw.w1 << 32) | hw.w0) >> sh);
+                        const u32 d1 = (u32)((((u64)hw.w2 << 32) | hw.w1) >> sh);
+                        const u32 d2 = (u32)((((u64)hw.w3 << 32) | hw.w2) >> sh);
+                        const u32 d3 = (u32)((((u64)hw.w4 << 32) | hw.w3) >> sh);
+                        u32 hdr, masked, key;
+                        bool ok;
+                        if ((d0 & S.fm[0]) == S.fe[0] && (d1 & S.fm[1]) == S.fe[1] && (d2 & S.fm[2]) == S.fe[2]) {
+                            ok = true;
+                            masked = 1;
+                            hdr = S.fhdr;
+                            key = S.f64 ? (d2 >> 16) | (d3 << 16) : d1;
+                        } else {
+                            ok = spec_match((u64)d0 | ((u64)d1 << 32), (u64)d2 | ((u64)d3 << 32), S, hdr, masked, key);
+                        }
+                        if (F >= 0) {                                               // this wave owns the header
+                            const bool second = (u32)j >= jb;
+                            if (!ok) {
+                                if (second) bad2 = true;
+                                else bad = true;
+                            } else if (lane == 0) {
+                                spec_store_desc(desc + (second ? dbase2 + (j - jb) : dbase + kA + j), pos, d0 & 0xFFu, hdr,
+                                                masked, gg);
+                            }
+                        }
+                        Pj[j] = F + (int)hdr;
+                        RK[j] = ok && masked ? rotl32(key, 8u * ((u32)(F + (int)hdr) & 3u)) : 0u;
+                    }
+                    if (bad && lane == 0) spec_flag(flags, list, head, s);
+                    if (bad2 && lane == 0) spec_flag(flags, list, head, s + 1);
+                    // the XOR rule per lane: its chunk's frame j (x >= F_j), whole-payload chunks
+                    // one XOR per dword, chunks holding header bytes byte-exact for frames j, j + 1
+#pragma unroll
+                    for (int u = 0; u < SPEC_U; ++u) {
+                        const int xx = u * 1024 + xl;
+                        const bool a1 = xx >= Fj[1], a2 = xx >= Fj[2];
+                        const int P = a2 ? Pj[2] : (a1 ? Pj[1] : Pj[0]);
+                        const int E = a2 ? Fj[2] + (int)gg : (a1 ? Fj[2] : Fj[1]);
+                        const u32 rk = a2 ? RK[2] : (a1 ? RK[1] : RK[0]);
+                        cov[u] = 0xFFFFu;
+                        if (xx >= P && xx + 16 <= E) {
+                            v[u].x ^= rk; v[u].y ^= rk; v[u].z ^= rk; v[u].w ^= rk;
+                        } else {
+                            u32 cdummy = 0;
+                            const int l1 = P > xx ? P - xx : 0, h1 = E < xx + 16 ? E - xx : 16;
+                            if (h1 > l1) ws_xor_range(rk, l1, h1, v[u], cdummy);
+                            const int Pn = a2 ? 0x40000000 : (a1 ? Pj[2] : Pj[1]);
+                            const u32 rkn = a2 ? 0u : (a1 ? RK[2] : RK[1]);
+                            if (Pn < xx + 16) ws_xor_range(rkn, Pn > xx ? Pn - xx : 0, 16, v[u], cdummy);
+                        }
+                    }
+                }
+            }
+        }
+        for (u32 it = 1; !fast && s < nseg; ++s, ++it) {
             if ((it & 63) == 0) {                                           // an unordered batch stores nothing:
                 const u32 cc = lane == 0 ? ld_agent(myrepl) : 0u;           // stop walking garbage early
                 if (__builtin_amdgcn_readfirstlane(cc) == 2) break;
@@ -360,7 +496,7 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
             }
             const u64 dbase = desc_base ? sld64(desc_base + s) : (u64)s * max_frames;
             bool bad = false;
-            for (u32 k = kA; DBG != 1 && fr < (int)RW; ++k, fr += (int)g) {
+            for (u32 k = kA; fr < (int)RW; ++k, fr += (int)g) {
                 const u64 rel = (u64)k * g, pos = so + rel;                 // segment- / buffer-relative
                 u64 w0, w1;
                 if (k >= nfull) {                                           // past the predicted frames: the
@@ -375,9 +511,9 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
                 const bool ok = spec_match(w0, w1, S, hdr, masked, key);
                 if (fr >= 0) {                                              // this wave owns the header
                     if (!ok) bad = true;
-                    else if (lane == 0 && DBG != 3) spec_store_desc(desc + dbase + k, pos, (u32)w0 & 0xFFu, hdr, masked, (u32)g);
+                    else if (lane == 0) spec_store_desc(desc + dbase + k, pos, (u32)w0 & 0xFFu, hdr, masked, (u32)g);
                 }
-                if (!ok || !masked || DBG == 2) continue;                   // the XOR rule
+                if (!ok || !masked) continue;                               // the XOR rule
                 const int qa = fr + (int)hdr, qb = fr + (int)g;
                 if (qb <= 0 || qa >= (int)RW) continue;
                 // (origin-relative payload start r0 + qa: the key rotated to the chunk phase)
@@ -386,7 +522,7 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
             }
             if (bad && lane == 0) spec_flag(flags, list, head, s);
         }
-        s_stop = s < nseg ? s + 1 : nseg;
+        if (!fast) s_stop = s < nseg ? s + 1 : nseg;
     }
     // ---- 4. wait for the checkers' verdict (bounded), then store
     if (lane == 0) {
@@ -412,9 +548,9 @@ __global__ __launch_bounds__(SPEC_T) void ws_piece_spec_kernel(
     }
 #pragma unroll
     for (int u = 0; u < SPEC_U; ++u) {
-        const u64 cidx = wc0 + (u64)(u * 64 + lane);
-        if (!cov[u] || (!inside && (cidx < c_lo || cidx >= c_hi))) continue;
-        gu32x4* const pc = wbase + (u * 64 + lane);
+        const int rel = u * 64 + (int)lane;
+        if (!cov[u] || rel < A || rel > B) continue;
+        gu32x4* const pc = reinterpret_cast<gu32x4*>(sbase + (u32)((rel - A) * 16));
         if (cov[u] == 0xFFFFu || allseg || segcov[u] == 0xFFFFu) st16<NT>(v[u], pc);
         else ws_store_bytes(reinterpret_cast<gu8*>(pc), v[u], cov[u]);
     }
@@ -586,15 +722,13 @@ int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, 
     const u32 nchk = (u32)(waves < 1024 ? waves : 1024);
     const u32 chk_per = (u32)((L.nseg + nchk - 1) / nchk);
     if (chk_per > 256) return ws_set_msg("spec decode: too many segments for the checkers");
-    const SpecSig S = spec_sig(g);
+    SpecSig S = spec_sig(g);
+    S.gs = (float)L.nseg * 256.0f / (float)(hi - lo);
     size_t tslot = 0;
     int rc;
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    const int dbg = ws_spec_dbg;
-    auto kern = dbg == 1 ? ws_piece_spec_kernel<1, 1> : dbg == 2 ? ws_piece_spec_kernel<1, 2> : dbg == 3 ? ws_piece_spec_kernel<1, 3>
-              : dbg == 4 ? ws_piece_spec_kernel<1, 4> : ws_piece_spec_kernel<1, 0>;
-    hipLaunchKernelGGL(kern, dim3((u32)grid), dim3(SPEC_T), ws_piece_dyn_lds(L), L.stream, L.buf,
+    hipLaunchKernelGGL(ws_piece_spec_kernel<1>, dim3((u32)grid), dim3(SPEC_T), ws_piece_dyn_lds(L), L.stream, L.buf,
                        L.seg_off, L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, head, done, flags, list,
                        marks, tag, pbase, c_lo, c_hi, lo, hi, ppw, npieces, wshift, nchk, chk_per,
                        (u32)(int)ws_spec_spins, S);
