@@ -150,7 +150,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
 // by the stream. A call pins its slot for its whole duration (WsSlot): LRU eviction never
 // takes a pinned slot. A graph capture's slot belongs to that graph: a HIP user object on the
 // graph marks it dead when the graph (and every executable made from it) is destroyed, and the
-// next library call frees its buffers.
+// next eager library call frees its buffers.
 #define WS_MAX_DEV 64
 #define WS_STREAM_SLOTS 16
 struct WsStreamWs {
@@ -272,9 +272,15 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
         cap = 0;
     else if (!cap)
         cap = ~0ull;
-    // release the slots of destroyed graphs
-    for (WsStreamWs& w : ds->sw)
-        if (w.used && w.captured && w.dead.load() && !w.busy) slot_free(w);
+    // release the slots of destroyed graphs, from eager calls only: a hipFree while this stream
+    // captures would invalidate the capture (relaxed mode for captures on other threads)
+    if (!cap) {
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        for (WsStreamWs& w : ds->sw)
+            if (w.used && w.captured && w.dead.load() && !w.busy) slot_free(w);
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+    }
     WsStreamWs* lru = nullptr;
     WsStreamWs* freeslot = nullptr;
     size_t eager = 0;
@@ -549,7 +555,8 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
         // as fast or faster: K1 costs little there, and K2 right behind K1 streams faster than
         // any one-pass kernel, profiles/r03_spec_sweep.log); forced: whenever it fits
         // (the device's advice and frame-length hint: adv_h[0], adv_h[1]; option spec_g overrides the hint)
-        int hint = ws_spec_g > 0 ? (int)ws_spec_g : __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED);
+        // (captured calls have no advice word and never speculate)
+        int hint = ws_spec_g > 0 ? (int)ws_spec_g : adv_h ? __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED) : 0;
         if (spec_opt == 2 && hint < 2) hint = 1024;     // forced with no hint yet: any length verifies
         if (!cap && spec_opt && hint >= 2 && hint < (1 << 30) && ws_spec_fits(hi - lo, nseg) &&
             (spec_opt == 2 || (__atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1 && hint >= WS_SPEC_ADAPT_G))) {
