@@ -1,0 +1,84 @@
+// tools/exp_k1k2.hip — experiment only (not part of the drop-in): why does K2 stream faster
+// right behind K1 than alone or than any plain in-place XOR of its shape? Linked against
+// the product's objects (internal launchers), built by tools/exp_k1k2.sh into
+// tools/libexp_k1k2.so. Sequences, each `iters` times on `stream` (after one K1 that leaves
+// the workspace in place):
+//   0  K1 + K2 (the product's classic step)
+//   1  K2 alone (the same items again)
+//   2  spin kernel (`arg` us, one block, no memory traffic) + K2
+//   3  header-line touch (32 B at every frame start, like K1's loads, no stores) + K2
+//   4  mid-frame touch (32 B at every frame start + arg bytes: lines K2 reads too) + K2
+//   5  touch of lines in another buffer (same count, not read by K2) + K2
+//   6  header-line touch alone      7  K1 alone      8  spin alone
+#include "../util_amd/csrc/ws_common.h"
+
+__global__ void exp_spin_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+// thread i loads 32 B at base + i*stride + off (clamped to n); the sum never matches the
+// run-time key, so nothing is stored, but the loads cannot be removed
+__global__ __launch_bounds__(256) void exp_touch_kernel(const unsigned char* __restrict__ base, unsigned long long n,
+                                                       unsigned long long count, unsigned long long stride,
+                                                       unsigned long long off, u32 key, u32* sink) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    unsigned long long a = i * stride + off;
+    if (a + 32 > n) a = n - 32;
+    const gu32x4* q = reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(base + a) & ~(uintptr_t)15);
+    const u32x4 x0 = q[0], x1 = q[1];
+    const u32 h = x0.x ^ x0.y ^ x0.z ^ x0.w ^ x1.x ^ x1.y ^ x1.z ^ x1.w;
+    if (h == key) *gptr<u32>(sink) = h;
+}
+
+extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
+    unsigned char* buf, unsigned long long buflen, const u64* seg_off, const u64* seg_len, unsigned int nseg,
+    unsigned int max_frames, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res, unsigned char* other,
+    unsigned long long other_len, unsigned long long nframes, unsigned long long stride, int mode, int iters,
+    long long arg, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    static unsigned char* ws = nullptr;
+    static size_t ws_bytes = 0;
+    static u32* sink = nullptr;
+    const size_t need = ws_piece_workspace_bytes(buflen, nseg, max_frames);
+    if (ws_bytes < need) {
+        if (ws) (void)hipFree(ws);
+        if (hipMalloc(&ws, need) != hipSuccess) return -2;
+        (void)hipMemset(ws, 0, need);
+        ws_bytes = need;
+    }
+    if (!sink && hipMalloc(&sink, 64) != hipSuccess) return -2;
+    int cus = 256, lds = 160 * 1024;
+    WsLaunch L;
+    L.buf = buf; L.seg_off = seg_off; L.seg_len = seg_len; L.nseg = nseg; L.max_frames = max_frames;
+    L.desc_base = nullptr; L.desc = desc; L.res = res; L.stream = st; L.cus = cus; L.lds_per_cu = lds;
+    static u32 gen = 100;
+    PieceWs P;
+    int rc = ws_launch_piece_scan(L, 0, buflen, ws, ++gen, &P);
+    if (rc) return rc;
+    const u32 tb = (u32)((nframes + 255) / 256);
+    const unsigned long long spin = (unsigned long long)(arg > 0 ? arg : 40) * 100;   // 100 MHz counter
+    for (int it = 0; it < iters; ++it) {
+        switch (mode) {
+        case 0: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc; break;
+        case 2: case 8: hipLaunchKernelGGL(exp_spin_kernel, dim3(1), dim3(64), 0, st, spin); break;
+        case 3: case 6:
+            hipLaunchKernelGGL(exp_touch_kernel, dim3(tb), dim3(256), 0, st, buf, buflen, nframes, stride, 0ull,
+                               0xA5A5F00Du, sink);
+            break;
+        case 4:
+            hipLaunchKernelGGL(exp_touch_kernel, dim3(tb), dim3(256), 0, st, buf, buflen, nframes, stride,
+                               (unsigned long long)arg, 0xA5A5F00Du, sink);
+            break;
+        case 5:
+            hipLaunchKernelGGL(exp_touch_kernel, dim3(tb), dim3(256), 0, st, other, other_len, nframes, stride, 0ull,
+                               0xA5A5F00Du, sink);
+            break;
+        case 7: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc; break;
+        default: break;
+        }
+        if (mode <= 5 && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}

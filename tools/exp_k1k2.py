@@ -1,0 +1,52 @@
+"""Why K2 streams faster right behind K1 (tools/exp_k1k2.hip): cfg2 batch, every sequence
+timed as one event region of `iters` steps, rounds interleaved. GPU box:
+    python tools/exp_k1k2.py [rounds] [iters]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import torch
+
+here = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(here))
+import bench  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+dev = torch.device("cuda", 0)
+wl = bench.Workload.make("cfg2", dev)
+lib = C.CDLL(os.path.join(here, "libexp_k1k2.so"))
+f = lib.exp_k1k2_run
+f.restype = C.c_int
+vp, u64 = C.c_void_p, C.c_ulonglong
+f.argtypes = [vp, u64, vp, vp, C.c_uint, C.c_uint, vp, vp, vp, u64, u64, u64, C.c_int, C.c_int, C.c_longlong, vp]
+other = torch.zeros(wl.wire_bytes, dtype=torch.uint8, device=dev)
+st = torch.cuda.current_stream()
+nframes = wl.nframes
+stride = 4104
+names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
+         6: "hdrtouch", 7: "K1", 8: "spin40"}
+seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
+buflen = wl.wire_bytes
+
+
+def run(mode, arg, it):
+    rc = f(wl.buf.data_ptr(), buflen, wl.seg_off.data_ptr(), wl.seg_len.data_ptr(), wl.nseg, wl.fps,
+           wl.desc.data_ptr(), wl.res.data_ptr(), other.data_ptr(), other.numel(), nframes, stride, mode, it, arg,
+           st.cuda_stream)
+    assert rc == 0, rc
+
+
+res = {}
+for r in range(rounds):
+    for mode, arg in seq:
+        run(mode, arg, 8)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run(mode, arg, iters)
+        e1.record()
+        torch.cuda.synchronize()
+        res.setdefault("%s(%d)" % (names[mode], arg), []).append(round(e0.elapsed_time(e1) / iters, 4))
+print(json.dumps(res))

@@ -337,6 +337,39 @@ __global__ __launch_bounds__(256) void ws_calib_wcu_kernel(gu32x4* __restrict__ 
         if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
 }
 
+// mode 900/901: K2's block shape (256 threads, each wave 4 KiB of consecutive chunks, two
+// windows) with only half of a wave's bytes in flight at a time: 900 = load half A, store
+// it, then load and store half B; 901 = load A, wait for it, load B, store A, store B (B's
+// loads overlap A's stores). `dyn` bytes of unused LDS cap blocks per CU.
+template <int PH>
+__global__ __launch_bounds__(256) void ws_calib_2ph_kernel(gu32x4* __restrict__ a, u64 n, u32 W, u64 ppw, u32 key) {
+    const u64 per = 1024, npieces = (n + per - 1) / per, last = n - 1;
+    const u64 piece = (u64)(blockIdx.x % W) * ppw + blockIdx.x / W;
+    if (piece >= npieces) return;
+    const u64 i = piece * per + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+    u32x4 v[2], w[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) v[u] = ld16<1>(a + min(i + 64u * u, last));
+    if (PH == 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 2; ++u) w[u] = ld16<1>(a + min(i + 128u + 64u * u, last));
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 2; ++u) w[u] = ld16<1>(a + min(i + 128u + 64u * u, last));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (i + 64u * u < n) st16<1>(v[u] ^ key, a + i + 64u * u);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+        if (i + 128u + 64u * u < n) st16<1>(w[u] ^ key, a + i + 128u + 64u * u);
+}
+
 // mode 89x: blocks of T threads, U chunks per lane, wave-contiguous, two windows, and
 // (SYNC) a block-level hand-off between the loads and the stores — wave 0 writes 64 words
 // to LDS, barrier, every lane reads one before storing (a block that shares one lookup of
@@ -681,6 +714,15 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         else hipLaunchKernelGGL(ws_calib_copyoff_kernel<8>, dim3((u32)np), dim3(256), 0, st, a8, b, n, 0x5A5A5A5Au);
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_calib_copyoff_kernel launch", e);
+    }
+    if (mode == 900 || mode == 901) {  // `blocks` = unused LDS bytes per block
+        const u32 W = 2u;
+        const u64 np = (n + 1023) / 1024, ppw = (np + W - 1) / W;
+        const u32 dyn = blocks > 0 && blocks <= 65536 ? (u32)blocks : 0u;
+        if (mode == 900) hipLaunchKernelGGL(ws_calib_2ph_kernel<0>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        else hipLaunchKernelGGL(ws_calib_2ph_kernel<1>, dim3((u32)(ppw * W)), dim3(256), dyn, st, a, n, W, ppw, 0x5A5A5A5Au);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : ws_set_err("ws_calib_2ph_kernel launch", e);
     }
     if (mode >= 890 && mode <= 895) {  // 890/891: 512 x 2 (no sync / sync); 892/893: 256 x 4; 894/895: 1024 x 1
         const u32 W = 2u;
