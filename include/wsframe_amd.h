@@ -215,13 +215,14 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * up at once, exercising its repair path), "spec_g" (0: the speculative kernel predicts
  * frames of the length the previous call on the stream saw first; >= 2 forces that length,
  * for tests of mispredictions), "piece_lds" (unused dynamic LDS per unmask block:
- * caps its blocks per CU; 0 = the CU's LDS / 5), "piece_win" (0..6: log2 of the windows the
+ * caps its blocks per CU; 0 = the CU's LDS / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
  * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
- * "stream_rw" / "stream_rw_cmax" / "stream_rounds" (raw stream: chunk-parallel walk, log2 of
- * its largest chunk 16..26, pass rounds of a captured call 1..64), "k2_timing" (see
+ * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream: chunk-parallel
+ * walk, log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
+ * call's chunk records linked in parallel 0/1), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);

@@ -127,9 +127,10 @@ def _streams():
     yield "random_long", wire, 1 << 15                        # quirks, unmasked frames, zero gaps
 
 
-@pytest.mark.parametrize("case", ["uniform", "runs", "random", "max_frames", "mixed_long", "mixed_long_max_frames",
-                                  "random_long"])
-def test_stream_decode_graph_replay(dev, case):
+@pytest.mark.parametrize("case,plink", [("uniform", 1), ("runs", 1), ("random", 1), ("max_frames", 1),
+                                        ("mixed_long", 1), ("mixed_long", 0), ("mixed_long_max_frames", 1),
+                                        ("mixed_long_max_frames", 0), ("random_long", 1), ("random_long", 0)])
+def test_stream_decode_graph_replay(dev, case, plink):
     """websocketframeStreamDecodeDevice captured in a graph: the pass loop's state lives on
     the device (no host reads), and on a long stream whose lengths keep changing the
     chunk-parallel walk runs on the device too (plan, candidate walks, linker), so the
@@ -141,8 +142,12 @@ def test_stream_decode_graph_replay(dev, case):
     desc = torch.zeros(mf * 32, dtype=torch.uint8, device=dev)
     res = torch.zeros(16, dtype=torch.uint8, device=dev)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        W.stream_decode_device(d, n, mf, desc, res)
+    W.set_option("stream_plink", plink)          # 0: the serial linker only (read at capture)
+    try:
+        with torch.cuda.graph(g):
+            W.stream_decode_device(d, n, mf, desc, res)
+    finally:
+        W.set_option("stream_plink", 1)
     ob = wire.copy()
     od, orr = oracle_segments(ob, [0], [n], mf)
     for rnd in range(3):

@@ -10,6 +10,7 @@
 //   4  mid-frame touch (32 B at every frame start + arg bytes: lines K2 reads too) + K2
 //   5  touch of lines in another buffer (same count, not read by K2) + K2
 //   6  header-line touch alone      7  K1 alone      8  spin alone
+//   9  K1 with the first-step stride guess `arg` + K2      10  that K1 alone
 #include "../util_amd/csrc/ws_common.h"
 
 __global__ void exp_spin_kernel(unsigned long long ticks) {
@@ -76,9 +77,10 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
                                0xA5A5F00Du, sink);
             break;
         case 7: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc; break;
+        case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
         default: break;
         }
-        if (mode <= 5 && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -16,7 +16,9 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 dev = torch.device("cuda", 0)
 wl = bench.Workload.make("cfg2", dev)
-lib = C.CDLL(os.path.join(here, "libexp_k1k2.so"))
+lib = C.CDLL(os.path.join(here, os.environ.get("EXP_LIB", "libexp_k1k2.so")))
+lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
+ldsv = [int(x) for x in os.environ.get("EXP_LDS", "0").split(",")]
 f = lib.exp_k1k2_run
 f.restype = C.c_int
 vp, u64 = C.c_void_p, C.c_ulonglong
@@ -26,8 +28,10 @@ st = torch.cuda.current_stream()
 nframes = wl.nframes
 stride = 4104
 names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
-         6: "hdrtouch", 7: "K1", 8: "spin40"}
+         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g"}
 seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
+if os.environ.get("EXP_MODES"):
+    seq = [tuple(int(y) for y in x.split(":")) for x in os.environ["EXP_MODES"].split(",")]
 buflen = wl.wire_bytes
 
 
@@ -40,6 +44,8 @@ def run(mode, arg, it):
 
 res = {}
 for r in range(rounds):
+  for lds in ldsv:
+    assert lib.websocketframeGpuSetOption(b"piece_lds", lds) == 0
     for mode, arg in seq:
         run(mode, arg, 8)
         torch.cuda.synchronize()
@@ -48,5 +54,5 @@ for r in range(rounds):
         run(mode, arg, iters)
         e1.record()
         torch.cuda.synchronize()
-        res.setdefault("%s(%d)" % (names[mode], arg), []).append(round(e0.elapsed_time(e1) / iters, 4))
+        res.setdefault("%s(%d)lds%d" % (names[mode], arg, lds), []).append(round(e0.elapsed_time(e1) / iters, 4))
 print(json.dumps(res))

@@ -33,7 +33,7 @@ extern WsOpt ws_enc_front;
 extern WsOpt ws_spec_spins;
 WsOpt ws_spec_g{0};        // "spec_g": the frame length the speculative path predicts with (0: the device's hint)
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
-extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds;
+extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
 
@@ -103,6 +103,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_rw_cmax")) {
         if (value < 16 || value > 26) return -1;
         ws_stream_rw_cmax = (int)value;
+    }
+    else if (!strcmp(name, "stream_plink")) {
+        if (value < 0 || value > 1) return -1;
+        ws_stream_plink = (int)value;
     }
     else if (!strcmp(name, "stream_rounds")) {
         if (value < 1 || value > 64) return -1;
@@ -574,7 +578,12 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     const u32 gen = ws_next_gen();
     const u32* disorder = nullptr;
     bool fallback = false;
-    if ((rc = ws_launch_piece(L, lo, hi, reinterpret_cast<unsigned char*>(ws), gen, adv_d, &disorder, &fallback)))
+    // K1's first-step stride guess: the previous call's first frame length, while the device
+    // advised that nearly every segment held frames of one length (eager calls only)
+    const u32 g0 = adv_h && __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1 ? (u32)__atomic_load_n(adv_h + 1, __ATOMIC_RELAXED)
+                                                                         : 0u;
+    if ((rc = ws_launch_piece(L, lo, hi, reinterpret_cast<unsigned char*>(ws), gen, adv_d, &disorder, &fallback,
+                              g0 >= 2 ? g0 : 0u)))
         return rc;
     // segments out of buffer order are decoded by K2's fallback; with no pieces to launch K2
     // on, a small gated walker grid does it (exits at once for ordered batches)

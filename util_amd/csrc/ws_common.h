@@ -17,8 +17,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // and every load becomes its own round trip).
 // the unmask kernel's unit (ws_piece.hip K2, also behind the raw-stream path): one-shot
 // 256-thread blocks over WS_PIECE_U KiB per wave, 2^WS_PIECE_SHIFT bytes per block
+#ifndef WS_PIECE_U
 #define WS_PIECE_U 4
 #define WS_PIECE_SHIFT 14                   // 16 KiB = 256 threads * WS_PIECE_U * 16 B
+#endif
 #define WS_GLOBAL __attribute__((address_space(1)))
 typedef WS_GLOBAL u32x4 gu32x4;
 typedef WS_GLOBAL u32 gu32;
@@ -377,7 +379,7 @@ struct PieceWs {          // ws_piece.hip workspace views after K1
     u64 npieces, pbase, c_lo, c_hi;
 };
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
-                         bool count_nonuniform = false);
+                         bool count_nonuniform = false, u32 g0 = 0);
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr);
 int ws_piece_dyn_lds(const WsLaunch& L);
 // the speculative piece path (ws_spec.hip): no K1; sws = the slot's spec workspace
@@ -418,7 +420,7 @@ struct WsSlot {
 };
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,
-                    const u32** disorder_out, bool* fallback_needed);
+                    const u32** disorder_out, bool* fallback_needed, u32 g0 = 0);
 // the batch decode with every segment inside [lo, hi) of buf (ws_api.hip); `ws`
 // (optional) is a caller-owned workspace of ws_decode_workspace_bytes() bytes whose
 // first 16 bytes were zeroed once after allocation, else the per-device one is used

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 WebsocketSegResult_t* __restrict__ res,
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
-                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32* nonuni) {
+                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32* nonuni,
+                                                                u32 g0) {
     static_assert(G == 16, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
@@ -86,7 +87,10 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
     const u64 tag = (u64)sc << 32;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(buf + so);
     if (active && gl == 0) put_ptrs(ptr, pbase, pend, s ? prev_end + lead0 : 0, sorg, tag);
-    u64 off = 0, g = 0, walked_end = sorg;
+    // g0: the stride guess of the first step (the host's hint, 0 = none): lane k parses off + k*g0
+    // at once; lane 0's frame is always the true first one, so a wrong guess costs nothing but
+    // its loads (code 1 at lane 0 takes the true length)
+    u64 off = 0, g = g0, walked_end = sorg;
     u32 nf = 0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
     bool nonu = false;                       // frames of another length than the first, or an error stop
@@ -341,7 +345,7 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
 // [lo, hi) of L.buf. count_nonuniform: K1 counts segments with frames of several lengths
 // for the K2 that follows (ws_launch_piece); other users pass false.
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
-                         bool count_nonuniform) {
+                         bool count_nonuniform, u32 g0) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     PieceWs P;
@@ -359,7 +363,8 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     const u32 blocks = (u32)(((u64)L.nseg * 16 + PSCAN_T - 1) / PSCAN_T);
     hipLaunchKernelGGL(ws_piece_scan_kernel<16>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
                        L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
-                       P.disorder, gen, P.pbase, lo, hi, count_nonuniform ? P.nonuni : nullptr);
+                       P.disorder, gen, P.pbase, lo, hi, count_nonuniform ? P.nonuni : nullptr,
+                       g0 < (1u << 31) ? g0 : 0u);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
     *out = P;
@@ -367,10 +372,11 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 }
 
 // "piece_lds": bytes of unused dynamic LDS per K2 (and speculative S1) block, which caps its
-// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 5 — K2 needs only 58 VGPRs
-// (8 waves/SIMD would fit) but streams best at 5 blocks per CU: cfg2 1.363-1.366 ms at 5
-// against 1.378-1.382 (6), 1.395-1.399 (7), 1.402-1.420 (8), 1.386-1.387 (4); cfg3 and cfg4
-// the same way (profiles/r02_k2_occupancy_ab.log). On gfx950 (160 KiB per CU) that is 32 KiB.
+// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 6 — K2 needs only 60 VGPRs
+// (8 waves/SIMD would fit) but streams best at 6 blocks per CU in round 3 (cfg2 K1 + K2
+// 1.355 ms at 6 against 1.375-1.378 at 4 and 5, 1.374 at 7, 1.40 at 8, interleaved in one
+// process on three boxes: profiles/r03_k2_occupancy.log; round 2's K2 was best at 5). On
+// gfx950 (160 KiB per CU) that is 27,136 B.
 WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
@@ -378,7 +384,7 @@ WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 
 int ws_piece_dyn_lds(const WsLaunch& L) {
     const int opt = ws_piece_lds;
     if (opt > 0) return opt <= 65536 ? opt : 65536;
-    const int per = L.lds_per_cu / 5;                       // 5 blocks per CU
+    const int per = L.lds_per_cu / 6;                       // 6 blocks per CU
     return per > 65536 ? 65536 : (per & ~255);
 }
 
@@ -447,9 +453,9 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
 // K1 + K2; K2 also holds the fallback for unordered batches. *fallback_needed: no K2
 // was launched (no pieces), so the caller must launch the gated walker itself.
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,
-                    const u32** disorder_out, bool* fallback_needed) {
+                    const u32** disorder_out, bool* fallback_needed, u32 g0) {
     PieceWs P;
-    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr);
+    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr, g0);
     if (rc) return rc;
     if ((rc = ws_launch_piece_unmask(L, P, gen, advice))) return rc;
     *disorder_out = P.disorder;

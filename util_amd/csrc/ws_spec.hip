@@ -46,7 +46,7 @@
 #define SPEC_U WS_PIECE_U
 #define SPEC_SHIFT WS_PIECE_SHIFT
 #define SPEC_FAST_G 2048                    // fast path: at most 3 frames touch a wave's range
-#define SPEC_RANGE_SHIFT 12                 // one wave's range: 64 lanes x SPEC_U x 16 B = 4 KiB
+#define SPEC_RANGE_SHIFT (SPEC_SHIFT - 2)   // one wave's range: 64 lanes x SPEC_U x 16 B = 4 KiB
 static_assert((1 << SPEC_RANGE_SHIFT) == 64 * SPEC_U * 16, "wave range");
 // bounded wait for the checkers (s_sleep 2 + a load each): option "spec_spins" (0 = give up
 // unless the first poll finds them done: exercises the repair path in tests)

@@ -761,6 +761,176 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     }
 }
 
+// ---- The captured call's linker, chunk-parallel (the common case; ws_rw_link_kernel below
+// stays as the exact serial fallback). The chain's entry into chunk c is the exit of chunk
+// c-1's owner walk on the chain; wrong starts inside a window either die (an implausible
+// header: owner dead) or merge with the chain, so the live owners of a chunk nearly always
+// agree on ONE exit, and then the entry into chunk c is known without the chain before it.
+// ws_rw_plink_kernel (one wavefront per chunk): entry = that common exit (chunk 0: the
+// plan's P), its record, its owner; ws_rw_pscan_kernel (one block): the frame counts'
+// prefix sum up to the first chunk that ends the walk, and the emit rows exactly as the
+// serial linker writes them. Anything else — live owners that disagree, an entry outside
+// its window or without a record or owner, a frame spanning a whole chunk, max_frames
+// reached before the chain's last chunk, no chunk ending the walk — leaves nrows at 0 and
+// the serial linker runs.
+struct RwLink {
+    u64 ent, rexit;
+    u32 cnt_w, nb, oi, flags;       // flags: 1 valid, 2 the walk ends in the window, 4 the chain ends here
+};
+
+__global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* __restrict__ plan,
+                                                         const RwRec* __restrict__ recs, const u32* __restrict__ nrec,
+                                                         const unsigned long long* __restrict__ dx,
+                                                         const RwOwn* __restrict__ own, RwLink* __restrict__ lk) {
+    const u32 lane = threadIdx.x, c = blockIdx.x;
+    if (!plan->active || c >= plan->nchunks) return;
+    const u64 P = plan->P, C = plan->C;
+    const u32 H = plan->H, nchunks = plan->nchunks;
+    const u64 cs0 = P + (u64)c * C;
+    const bool lastc = c + 1 == nchunks;
+    auto rl64 = [](u64 v, int i) -> u64 {
+        return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, i) |
+               ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), i) << 32);
+    };
+    // the entry: the common exit of chunk c-1's live owners
+    u64 ent = P;
+    bool ok = true;
+    if (c) {
+        const u64 oi = (u64)(c - 1) * RW_D + (lane & (RW_D - 1));
+        const u64 d = dx[oi];
+        const RwOwn o = own[oi];
+        const bool live = lane < RW_D && d != 0 && !o.dead;
+        const u64 m = __ballot(live);
+        if (!m) {
+            ok = false;
+        } else {
+            ent = rl64(o.exit, __builtin_ctzll(m));
+            ok = __ballot(live && o.exit != ent) == 0;
+        }
+    }
+    ok = ok && ent >= cs0 && ent - cs0 < H && (lastc || ent - cs0 < C);
+    RwLink L = {ent, 0, 0, 0, 0, 0};
+    if (ok) {
+        const u32 so = (u32)(ent - cs0);
+        const u32 n0 = nrec[4 * (u64)c], n1 = nrec[4 * (u64)c + 1];
+        const u32 na = n0 < RW_S0 ? n0 : RW_S0;
+        const RwRec q = recs[(u64)c * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
+        u64 m = __ballot(lane < na && q.start == so);
+        u32 rcs = 0;
+        u64 rexit = 0;
+        bool found = false;
+        if (m) {
+            const int i = __builtin_ctzll(m);
+            rcs = (u32)__builtin_amdgcn_readlane((int)q.cs, i);
+            rexit = rl64(q.exit, i);
+            found = true;
+        } else {                                                             // walks that end the stream
+            const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + (u64)c * RW_SLOTS + RW_S0;
+            const u32 nb1 = lastc ? (n1 < RW_SLAST ? n1 : RW_SLAST) : (n1 < RW_S1 ? n1 : RW_S1);
+            for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
+                RwRec q1 = {};
+                if (k0 + lane < nb1) q1 = r1[k0 + lane];
+                const u64 m1 = __ballot(k0 + lane < nb1 && q1.start == so);
+                if (m1) {
+                    const int i = __builtin_ctzll(m1);
+                    rcs = (u32)__builtin_amdgcn_readlane((int)q1.cs, i);
+                    rexit = rl64(q1.exit, i);
+                    found = true;
+                }
+            }
+        }
+        if (found) {
+            L.cnt_w = rcs & 0x7FFFFFFFu;
+            L.rexit = rexit;
+            if (rcs >> 31) {
+                L.flags = 1 | 2 | 4;                                         // the walk ends in the window
+            } else {
+                const u64 oi = (u64)c * RW_D + (lane & (RW_D - 1));
+                const u64 d = dx[oi];
+                const RwOwn o = own[oi];
+                const u64 mo = __ballot(lane < RW_D && d == rexit);
+                if (mo) {
+                    const int i = __builtin_ctzll(mo);
+                    const u32 dead = (u32)__builtin_amdgcn_readlane((int)o.dead, i);
+                    const u32 ocs = (u32)__builtin_amdgcn_readlane((int)o.cs, i);
+                    const u64 oexit = rl64(o.exit, i);
+                    const bool ends = (ocs >> 31) != 0 || oexit >= len;
+                    if (!dead && (ends || (oexit >= cs0 + C && oexit - cs0 < 2 * C && !lastc))) {
+                        L.nb = ocs & 0x7FFFFFFFu;
+                        L.oi = (u32)((u64)c * RW_D + (u64)i);
+                        L.flags = 1 | (ends ? 4 : 0);
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) lk[c] = L;
+}
+
+// one block of RW_PS_T threads: the prefix sum of the chain's frame counts and the emit rows
+#define RW_PS_T 1024
+__global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, RwPlan* __restrict__ plan,
+                                                             const RwLink* __restrict__ lk, u64* __restrict__ tab) {
+    __shared__ u32 s_stop;
+    __shared__ u32 s_bad;
+    __shared__ u64 s_wsum[RW_PS_T / 64];
+    __shared__ u64 s_carry;
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (!plan->active) return;
+    const u32 nchunks = plan->nchunks, stgn = plan->stgn;
+    if (tid == 0) { s_stop = nchunks; s_bad = 0; s_carry = plan->nf; }
+    __syncthreads();
+    // the first chunk that is invalid or ends the chain
+    for (u32 c = tid; c < nchunks; c += RW_PS_T) {
+        const u32 f = lk[c].flags;
+        if (!(f & 1) || (f & 4)) atomicMin(&s_stop, c);
+    }
+    __syncthreads();
+    const u32 stop = s_stop;
+    if (stop >= nchunks || !(lk[stop].flags & 1)) return;                   // the serial linker runs
+    // frame counts of chunks [0, stop): nfc before each, max_frames never reached on the way
+    for (u32 t0 = 0; t0 <= stop; t0 += RW_PS_T) {
+        const u32 c = t0 + tid;
+        RwLink L = {};
+        if (c <= stop) L = lk[c];
+        const u64 cnt = c < stop ? (u64)L.cnt_w + L.nb : 0;
+        u64 x = cnt;                                                         // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u64 y = (u64)__shfl_up((long long)x, d);
+            if (lane >= (u32)d) x += y;
+        }
+        if (lane == 63) s_wsum[wv] = x;
+        __syncthreads();
+        u64 before = s_carry;
+        for (u32 w = 0; w < wv; ++w) before += s_wsum[w];
+        const u64 nfc = before + x - cnt;
+        if (c < stop) {
+            if (nfc + cnt >= max_frames) s_bad = 1;                         // max_frames mid-chain: serial
+            u64* t = tab + 8 * (u64)c;
+            const u64 n_par = L.nb < stgn ? L.nb : stgn;
+            t[0] = L.ent; t[1] = L.rexit; t[2] = nfc; t[3] = L.cnt_w; t[4] = L.oi; t[5] = n_par; t[6] = 0;
+            t[7] = plan->P + (u64)c * plan->C;
+        } else if (c == stop) {
+            u64* t = tab + 8 * (u64)c;
+            const u64 cs0 = plan->P + (u64)c * plan->C;
+            if ((L.flags & 2) || nfc + L.cnt_w >= max_frames) {             // ends in the window: group walk
+                t[0] = L.ent; t[1] = 0; t[2] = nfc; t[3] = 0; t[4] = ~0ull; t[5] = 0; t[6] = 1; t[7] = cs0;
+            } else {
+                u64 n_par = L.nb < stgn ? L.nb : stgn;
+                if (nfc + L.cnt_w + n_par > max_frames) n_par = max_frames - nfc - L.cnt_w;
+                t[0] = L.ent; t[1] = L.rexit; t[2] = nfc; t[3] = L.cnt_w; t[4] = L.oi; t[5] = n_par; t[6] = 1;
+                t[7] = cs0;
+            }
+        }
+        __syncthreads();
+        if (tid == RW_PS_T - 1) s_carry = before + x;
+        __syncthreads();
+    }
+    if (tid == 0 && !s_bad) plan->nrows = stop + 1;
+}
+
+
 // The linker: from the plan's entry, chunk by chunk, the record whose start is the entry
 // (A records, then the walks that end the stream), its window exit's owner walk, one
 // emit row per chunk; a chunk without a usable record is walked here by this wavefront
@@ -775,7 +945,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
     const u32 lane = threadIdx.x;
-    if (!plan->active) return;
+    if (!plan->active || plan->nrows) return;                                // linked by ws_rw_pscan_kernel
     const u64 P = plan->P, C = plan->C;
     const u32 H = plan->H, nchunks = plan->nchunks, stgn = plan->stgn;
     u64 ent = P;
@@ -899,6 +1069,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
 WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
+WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
 
@@ -1094,7 +1265,7 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
 // geometry chosen on the device (ws_rw_plan_kernel). Layout after the aux head.
 struct RwDevLayout {
     u64 cmin, nch_cap, cand_cap, stg_cap;
-    size_t o_plan, o_recs, o_nrec, o_dx, o_own, o_tab, o_stg, o_cand, bytes, zero_bytes;
+    size_t o_plan, o_recs, o_nrec, o_dx, o_own, o_tab, o_stg, o_cand, o_lk, bytes, zero_bytes;
 };
 static RwDevLayout rw_dev_layout(u64 len) {
     RwDevLayout L;
@@ -1114,6 +1285,7 @@ static RwDevLayout rw_dev_layout(u64 len) {
     L.o_tab = o; o += up((L.nch_cap + 2) * 64);
     L.o_stg = o; o += up(L.stg_cap * 4);
     L.o_cand = o; o += up(L.cand_cap * 8);
+    L.o_lk = o; o += up(L.nch_cap * sizeof(RwLink));
     L.bytes = o;
     return L;
 }
@@ -1142,6 +1314,12 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
                        (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
+    if (ws_stream_plink) {          // the chunk-parallel linker; the serial one below exits if it linked
+        RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
+        hipLaunchKernelGGL(ws_rw_plink_kernel, dim3((u32)L.nch_cap), dim3(64), 0, st, len, (const RwPlan*)plan,
+                           (const RwRec*)recs, (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, lk);
+        hipLaunchKernelGGL(ws_rw_pscan_kernel, dim3(1), dim3(RW_PS_T), 0, st, max_frames, plan, (const RwLink*)lk, tab);
+    }
     hipLaunchKernelGGL(ws_rw_link_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, plan, (const RwRec*)recs,
                        (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, tab, d_desc, Pw.items,
                        Pw.ptr, Pw.npieces, Pw.nwork, d_res);
