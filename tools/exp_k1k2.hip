@@ -11,11 +11,25 @@
 //   5  touch of lines in another buffer (same count, not read by K2) + K2
 //   6  header-line touch alone      7  K1 alone      8  spin alone
 //   9  K1 with the first-step stride guess `arg` + K2      10  that K1 alone
+//   11 latency-bound chase kernel (arg % 1000 x 10 us; 256 blocks if arg > 1000, else 1) + K2   12 it alone
 #include "../util_amd/csrc/ws_common.h"
 
 __global__ void exp_spin_kernel(unsigned long long ticks) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+// one block of 256 threads: dependent random loads over the buffer until `ticks` (100 MHz)
+// have passed (a latency-bound, low-activity kernel like the raw stream's walks)
+__global__ __launch_bounds__(256) void exp_chase_kernel(const u32* __restrict__ a, unsigned long long n4,
+                                                       unsigned long long ticks, u32* sink) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    u32 x = threadIdx.x * 2654435761u;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+        const unsigned long long i = ((unsigned long long)(x * 2654435761u) * 64ull) % n4;
+        x += a[i] | 1u;
+    }
+    if (x == 0x12345678u) *gptr<u32>(sink) = x;
 }
 
 // thread i loads 32 B at base + i*stride + off (clamped to n); the sum never matches the
@@ -77,10 +91,15 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
                                0xA5A5F00Du, sink);
             break;
         case 7: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc; break;
+        case 11: case 12:
+            hipLaunchKernelGGL(exp_chase_kernel, dim3(arg > 1000 ? 256 : 1), dim3(256), 0, st,
+                               reinterpret_cast<const u32*>(buf), buflen / 4, (unsigned long long)(arg % 1000) * 100 * 10,
+                               sink);
+            break;
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
         default: break;
         }
-        if ((mode <= 5 || mode == 9) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9 || mode == 11) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

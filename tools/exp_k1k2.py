@@ -28,7 +28,7 @@ st = torch.cuda.current_stream()
 nframes = wl.nframes
 stride = 4104
 names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
-         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g"}
+         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase"}
 seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
 if os.environ.get("EXP_MODES"):
     seq = [tuple(int(y) for y in x.split(":")) for x in os.environ["EXP_MODES"].split(",")]

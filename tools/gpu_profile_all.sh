@@ -3,8 +3,8 @@
 #   bash tools/gpu_profile_all.sh r02 [names...]
 set -e
 export TMPDIR=/tmp
-R=${1:-r02}; shift || true
-ALL="piece piece_cfg3 piece_cfg4 segfuse_cfg5 reasm_fused encode_cfg2 stream_cfg2 stream_cfg3"
+R=${1:-r03}; shift || true
+ALL="piece piece_cfg3 piece_cfg4 segfuse_cfg5 reasm_fused encode_cfg2 stream_cfg2 stream_cfg3 stream_cfg3_graph"
 for n in ${@:-$ALL}; do
   case $n in
     piece)        bash tools/profile.sh gpurun_out/${R}_piece ;;
@@ -15,6 +15,7 @@ for n in ${@:-$ALL}; do
     encode_cfg2)  bash tools/profile.sh gpurun_out/${R}_encode_cfg2 --op encode ;;
     stream_cfg2)  bash tools/profile.sh gpurun_out/${R}_stream_cfg2 --op stream --config cfg2 ;;
     stream_cfg3)  bash tools/profile.sh gpurun_out/${R}_stream_cfg3 --op stream --config cfg3 --steps 20 --warmup 3 ;;
+    stream_cfg3_graph) bash tools/profile.sh gpurun_out/${R}_stream_cfg3_graph --op stream --config cfg3 --graph --steps 20 --warmup 3 ;;
   esac
   echo "== $n"; cut -c1-200 gpurun_out/${R}_$n/bench.json
 done

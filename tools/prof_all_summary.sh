@@ -1,9 +1,9 @@
 # CPU side: profiles/<R>_* summaries from gpurun_out/<R>_* (tools/gpu_profile_all.sh)
 #   bash tools/prof_all_summary.sh r02
 set -e
-R=${1:-r02}
+R=${1:-r03}
 K2=ws_piece_unmask_kernel
-S() { [ -d gpurun_out/${R}_$1 ] && python tools/prof_summary.py gpurun_out/${R}_$1 ${R}_$1 --kernel $2 > /dev/null && echo "${R}_$1"; }
+S() { if [ -d gpurun_out/${R}_$1 ]; then python tools/prof_summary.py gpurun_out/${R}_$1 ${R}_$1 --kernel $2 > /dev/null && echo "${R}_$1"; fi; }
 S piece $K2,ws_piece_scan_kernel
 S piece_cfg3 $K2,ws_piece_scan_kernel
 S piece_cfg4 $K2,ws_piece_scan_kernel
@@ -12,3 +12,4 @@ S reasm_fused ws_reasm_seg_kernel
 S encode_cfg2 ws_enc_copy_kernel,ws_enc_front_kernel,ws_enc_tsum_kernel,ws_enc_tscan_kernel,ws_enc_edge_kernel,ws_enc_ptr_kernel
 S stream_cfg2 $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel
 S stream_cfg3 $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel,ws_rw_own_kernel,ws_rw_cand_kernel,ws_rw_spec_kernel,ws_rw_emit_kernel,ws_rw_chunk_kernel,ws_stream_finish_kernel
+S stream_cfg3_graph $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel,ws_rw_plan_kernel,ws_rw_own_kernel,ws_rw_cand_kernel,ws_rw_spec_kernel,ws_rw_plink_kernel,ws_rw_pscan_kernel,ws_rw_link_kernel,ws_rw_emit_kernel

@@ -10,7 +10,8 @@ Inputs (written by tools/profile.sh on the GPU box):
   <dir>/pmc_write/run_counter_collection.csv   rocprofv3 --pmc WRITE_SIZE
   <dir>/bench.json                        the bench line of the same code
 Outputs: profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_pmc.json,
-profiles/<tag>_bench.json.
+profiles/<tag>_bench.json (the traced run's own line), profiles/<tag>_bench_full.json (an
+untraced run with the CPU baseline and end-to-end fields).
 
 HBM traffic per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are
 in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
@@ -91,7 +92,19 @@ def main():
         rf["traffic_kernels"] = names
         if "per_kernel_ns_profiled" in rf:
             rf["per_kernel_ns_profiled"] = rec["per_kernel_avg_ns"]
+    # consistency: the step's kernels (each launched once per step) against the bench line of
+    # the same traced process — a kernel cannot take longer than the step that contains it
+    ks = [v["avg_ns"] for v in per_kernel.values() if v["avg_ns"] is not None]
+    rec["rocprof_kernel_sum_ms"] = round(sum(ks) / 1e6, 4) if ks else None
+    rec["same_run_ms_per_step"] = bench.get("ms_per_step")
+    if ks and bench.get("ms_per_step"):
+        rec["kernel_sum_le_step"] = sum(ks) / 1e6 <= bench["ms_per_step"]
+        rec["kernel_sum_frac_of_step"] = round(sum(ks) / 1e6 / bench["ms_per_step"], 4)
+    rec["bench_source"] = "the JSON line printed by the rocprofv3 --kernel-trace run itself (tools/profile.sh)"
     json.dump(rec, open(os.path.join(out, tag + "_pmc.json"), "w"), indent=1)
+    full = os.path.join(src, "bench_full.json")
+    if os.path.exists(full) and os.path.getsize(full):
+        shutil.copy(full, os.path.join(out, tag + "_bench_full.json"))
     json.dump(bench, open(os.path.join(out, tag + "_bench.json"), "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
