@@ -103,3 +103,102 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// The raw-stream path's K2 again on the workspace the stream call just left (same items,
+// pointers and segment pair): `iters` K2 launches after one websocketframeStreamDecodeDevice
+// call (mode 0), or that call alone `iters` times (mode 1). Isolates the stream K2's
+// +6 % over the batch K2 on cfg3: context (what runs before it) or inputs (what it reads).
+// thread i loads 32 B at base + offs[i] (the frame starts: what K1's header loads touch)
+__global__ __launch_bounds__(256) void exp_touch_idx_kernel(const unsigned char* __restrict__ base,
+                                                           const unsigned long long* __restrict__ offs,
+                                                           unsigned long long count, u32 key, u32* sink) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const gu32x4* q = reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(base + offs[i]) & ~(uintptr_t)15);
+    const u32x4 x0 = q[0], x1 = q[1];
+    const u32 h = x0.x ^ x0.y ^ x0.z ^ x0.w ^ x1.x ^ x1.y ^ x1.z ^ x1.w;
+    if (h == key) *gptr<u32>(sink) = h;
+}
+
+extern "C" int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len, unsigned int max_frames,
+                                                WebsocketFrameDesc_t* d_desc, WebsocketSegResult_t* d_res,
+                                                void* hip_stream);
+extern "C" __attribute__((visibility("default"))) int exp_stream_k2(unsigned char* buf, unsigned long long len,
+                                                                   unsigned int max_frames, WebsocketFrameDesc_t* desc,
+                                                                   WebsocketSegResult_t* res, int mode, int iters,
+                                                                   const unsigned long long* frame_off,
+                                                                   unsigned long long nframes, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    if (mode == 1) {
+        for (int i = 0; i < iters; ++i) {
+            const int rc = websocketframeStreamDecodeDevice(buf, len, max_frames, desc, res, hip_stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    int rc = websocketframeStreamDecodeDevice(buf, len, max_frames, desc, res, hip_stream);
+    if (rc) return rc;
+    const size_t pws = ws_piece_workspace_bytes(len, 1, max_frames);
+    void* ws = nullptr;
+    WsSlot slot;
+    if ((rc = slot.acquire(st)) || (rc = slot.workspace(pws + 64, 16, &ws))) return rc;
+    unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
+    u64* d_seg = reinterpret_cast<u64*>(w8 + ((pws + 15) & ~(size_t)15));
+    WsLaunch L;
+    L.buf = buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
+    L.desc_base = nullptr; L.desc = desc; L.res = res; L.stream = st;
+    L.cus = slot.cus; L.lds_per_cu = slot.lds;
+    PieceWs Pw;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    Pw.npieces = len + lead0 ? ((len + lead0 - 1) >> WS_PIECE_SHIFT) + 1 : 0;
+    Pw.pbase = 0;
+    Pw.c_lo = 0;
+    Pw.c_hi = (len + lead0 + 15) >> 4;
+    Pw.disorder = reinterpret_cast<u32*>(w8);
+    Pw.nonuni = reinterpret_cast<u32*>(w8) + 1;
+    Pw.ptr = reinterpret_cast<u64*>(w8 + 16);
+    size_t b = (16 + Pw.npieces * 8 + 15) & ~(size_t)15;
+    Pw.nwork = reinterpret_cast<u32*>(w8 + b);
+    b = (b + 4 + 15) & ~(size_t)15;
+    Pw.items = reinterpret_cast<u32x4*>(w8 + b);
+    static u32* sink = nullptr;
+    if (!sink && hipMalloc(&sink, 64) != hipSuccess) return -2;
+    for (int i = 0; i < iters; ++i) {
+        if (mode == 2)                          // the frame starts touched first (K1's header lines)
+            hipLaunchKernelGGL(exp_touch_idx_kernel, dim3((u32)((nframes + 255) / 256)), dim3(256), 0, st, buf,
+                               frame_off, nframes, 0xA5A5F00Du, sink);
+        if ((rc = ws_launch_piece_unmask(L, Pw, 0x7FFFFFF1u))) return rc;
+    }
+    return 0;
+}
+
+// batch: K1 once, then (frame-start touch + K2) x iters
+extern "C" __attribute__((visibility("default"))) int exp_batch_touch_k2(
+    unsigned char* buf, unsigned long long buflen, const u64* seg_off, const u64* seg_len, unsigned int nseg,
+    unsigned int max_frames, WebsocketFrameDesc_t* desc, WebsocketSegResult_t* res,
+    const unsigned long long* frame_off, unsigned long long nframes, int iters, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    static unsigned char* ws = nullptr;
+    static size_t ws_bytes = 0;
+    static u32* sink = nullptr;
+    const size_t need = ws_piece_workspace_bytes(buflen, nseg, max_frames);
+    if (ws_bytes < need) {
+        if (ws) (void)hipFree(ws);
+        if (hipMalloc(&ws, need) != hipSuccess) return -2;
+        (void)hipMemset(ws, 0, need);
+        ws_bytes = need;
+    }
+    if (!sink && hipMalloc(&sink, 64) != hipSuccess) return -2;
+    WsLaunch L;
+    L.buf = buf; L.seg_off = seg_off; L.seg_len = seg_len; L.nseg = nseg; L.max_frames = max_frames;
+    L.desc_base = nullptr; L.desc = desc; L.res = res; L.stream = st; L.cus = 256; L.lds_per_cu = 160 * 1024;
+    PieceWs P;
+    int rc = ws_launch_piece_scan(L, 0, buflen, ws, 77, &P);
+    if (rc) return rc;
+    for (int i = 0; i < iters; ++i) {
+        hipLaunchKernelGGL(exp_touch_idx_kernel, dim3((u32)((nframes + 255) / 256)), dim3(256), 0, st, buf, frame_off,
+                           nframes, 0xA5A5F00Du, sink);
+        if ((rc = ws_launch_piece_unmask(L, P, 77))) return rc;
+    }
+    return 0;
+}

@@ -616,7 +616,8 @@ __global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __
 
 // R3 (chunk walks): one lane per claimed window exit, the walk to the chunk's end; the
 // offsets of the frames it passes go to the staging list (the emit writes them in parallel)
-__global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
+#define RW_OWN_T 64       // one wavefront per block: the owner walks spread over every CU
+__global__ __launch_bounds__(RW_OWN_T) void ws_rw_own_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
                                                         u32 nchunks, u32 need_mask,
                                                         const unsigned long long* __restrict__ dx,
                                                         RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn,
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(256) void ws_rw_own_kernel(const unsigned char* __r
         if (!plan->active) return;
         P = plan->P; C = plan->C; nchunks = plan->nchunks; need_mask = plan->need_mask; stgn = plan->stgn;
     }
-    const u64 oi = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 oi = (u64)blockIdx.x * RW_OWN_T + threadIdx.x;
     if (oi >= (u64)nchunks * RW_D) return;
     u64 pos = dx[oi];
     if (!pos) return;
@@ -1183,7 +1184,7 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
                        need_mask, cand, capc, recs, nrec, dx, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
-    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len, P,
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len, P,
                        C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -1312,7 +1313,7 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
                        cand, nrec, 0u, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
-    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + 255) / 256)), dim3(256), 0, st, d_buf, len,
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len,
                        (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
     if (ws_stream_plink) {          // the chunk-parallel linker; the serial one below exits if it linked
         RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
