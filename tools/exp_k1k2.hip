@@ -11,6 +11,8 @@
 //   5  touch of lines in another buffer (same count, not read by K2) + K2
 //   6  header-line touch alone      7  K1 alone      8  spin alone
 //   9  K1 with the first-step stride guess `arg` + K2      10  that K1 alone
+//   13 K1 + plain XOR of `arg` MiB of another buffer + K2   14 read the workspace (items, pointers) + K2
+//   15 K1 twice + K2
 //   11 latency-bound chase kernel (arg % 1000 x 10 us; 256 blocks if arg > 1000, else 1) + K2   12 it alone
 #include "../util_amd/csrc/ws_common.h"
 
@@ -30,6 +32,27 @@ __global__ __launch_bounds__(256) void exp_chase_kernel(const u32* __restrict__ 
         x += a[i] | 1u;
     }
     if (x == 0x12345678u) *gptr<u32>(sink) = x;
+}
+
+// in-place XOR of n16 16-B chunks (a plain stream that evicts the caches)
+__global__ __launch_bounds__(256) void exp_xor_kernel(gu32x4* __restrict__ a, unsigned long long n16) {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n16;
+         i += (unsigned long long)gridDim.x * 256) {
+        u32x4 v = a[i];
+        v.x ^= 0x5A5A5A5Au; v.y ^= 0x5A5A5A5Au; v.z ^= 0x5A5A5A5Au; v.w ^= 0x5A5A5A5Au;
+        a[i] = v;
+    }
+}
+
+// read every 16-B entry of [p, p + n16) (the items / piece pointers K2 will read)
+__global__ __launch_bounds__(256) void exp_read_kernel(const gu32x4* __restrict__ a, unsigned long long n16, u32* sink) {
+    u32 h = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n16;
+         i += (unsigned long long)gridDim.x * 256) {
+        const u32x4 v = a[i];
+        h ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (h == 0xA5A5F00Du) *gptr<u32>(sink) = h;
 }
 
 // thread i loads 32 B at base + i*stride + off (clamped to n); the sum never matches the
@@ -96,10 +119,25 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
                                reinterpret_cast<const u32*>(buf), buflen / 4, (unsigned long long)(arg % 1000) * 100 * 10,
                                sink);
             break;
+        case 13:                                // K1, then a plain XOR of arg MiB of `other`, then K2
+            if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
+            hipLaunchKernelGGL(exp_xor_kernel, dim3(4096), dim3(256), 0, st,
+                               reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(other)),
+                               (unsigned long long)arg << 16);
+            break;
+        case 14:                                // read the items + piece pointers, then K2
+            hipLaunchKernelGGL(exp_read_kernel, dim3(2048), dim3(256), 0, st,
+                               reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(ws)),
+                               (unsigned long long)(need / 16), sink);
+            break;
+        case 15:                                // K1 twice, then K2
+            if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
+            if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
+            break;
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
         default: break;
         }
-        if ((mode <= 5 || mode == 9 || mode == 11) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9 || mode == 11 || mode >= 13) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -15,7 +15,7 @@ import bench  # noqa: E402
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 dev = torch.device("cuda", 0)
-wl = bench.Workload.make("cfg2", dev)
+wl = bench.Workload.make(os.environ.get("EXP_CFG", "cfg2"), dev)
 lib = C.CDLL(os.path.join(here, os.environ.get("EXP_LIB", "libexp_k1k2.so")))
 lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
 ldsv = [int(x) for x in os.environ.get("EXP_LDS", "0").split(",")]
@@ -26,9 +26,9 @@ f.argtypes = [vp, u64, vp, vp, C.c_uint, C.c_uint, vp, vp, vp, u64, u64, u64, C.
 other = torch.zeros(wl.wire_bytes, dtype=torch.uint8, device=dev)
 st = torch.cuda.current_stream()
 nframes = wl.nframes
-stride = 4104
+stride = int(os.environ.get("EXP_STRIDE", "4104"))
 names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
-         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase"}
+         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase", 13: "K1+xor+K2", 14: "wsread+K2", 15: "K1K1+K2"}
 seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
 if os.environ.get("EXP_MODES"):
     seq = [tuple(int(y) for y in x.split(":")) for x in os.environ["EXP_MODES"].split(",")]
