@@ -209,7 +209,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
  * configuration; every value yields bit-identical results, each one is parity-tested in
  * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_spec"
- * (path 3: 0 always the scan kernel + unmask, 1 adaptive — speculative, with no scan kernel,
+ * (path 3: 0 always the scan kernel + unmask (default), 1 adaptive — speculative, with no scan kernel,
  * when the previous eager call on the stream advised it — 2 speculative whenever the batch
  * fits), "spec_spins" (the speculative kernel's bounded wait for its table checkers; 0 gives
  * up at once, exercising its repair path), "spec_g" (0: the speculative kernel predicts

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-DEFAULTS = {"path": -1, "piece_spec": 1, "spec_g": 0, "spec_spins": 2048, "host_chunk_mb": 64, "piece_lds": 0,
+DEFAULTS = {"path": -1, "piece_spec": 0, "spec_g": 0, "spec_spins": 2048, "host_chunk_mb": 64, "piece_lds": 0,
             "piece_win": 1, "seg_win": 1, "reasm_path": 0, "reasm_cfg": 0, "enc_front": 1, "stream_rw": 1,
             "stream_rw_cmax": 23, "stream_rounds": 4, "stream_plink": 1, "k2_timing": 0}
 

@@ -29,14 +29,14 @@ def dev():
 # speculative form when the previous call on the stream advised it), 3 the classic piece path
 # (scan kernel + one-shot 16 KiB piece unmask), 5 = path 3 forced speculative (no scan kernel,
 # ws_spec.hip), 4 one workgroup per segment (segfuse)
-@pytest.fixture(params=[(-1, 1), (3, 0), (3, 2), (4, 1)], ids=["auto", "piece", "spec", "segfuse"], autouse=True)
+@pytest.fixture(params=[(-1, 0), (3, 1), (3, 2), (4, 0)], ids=["auto", "piece", "spec", "segfuse"], autouse=True)
 def decode_path(request):
     path, spec = request.param
     W.set_option("path", path)
     W.set_option("piece_spec", spec)
     yield 5 if spec == 2 else path
     W.set_option("path", -1)
-    W.set_option("piece_spec", 1)
+    W.set_option("piece_spec", 0)
 
 
 def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):

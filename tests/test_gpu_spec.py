@@ -31,7 +31,7 @@ def forced_spec():
     W.set_option("piece_spec", 2)
     yield
     W.set_option("path", -1)
-    W.set_option("piece_spec", 1)
+    W.set_option("piece_spec", 0)
     W.set_option("spec_spins", 2048)
     W.set_option("spec_g", 0)
 
@@ -274,7 +274,7 @@ def test_adaptive_choice(dev):
     advises the speculative path for a batch of equal frames of >= 48 KiB; a batch of mixed
     lengths makes the repair kernel advise the scan kernel again; equal frames below 48 KiB
     stay on the scan kernel (profiles/r03_spec_sweep.log). Every call bit-exact."""
-    W.set_option("piece_spec", 1)
+    W.set_option("piece_spec", 0)
     W.set_option("spec_g", 0)
     rng = np.random.default_rng(60)
     stream = torch.cuda.Stream(dev)

@@ -56,8 +56,11 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 static WsOpt g_path{-1};   // "path": -1 auto (4 for many small segments, else 3), 1 walker (one wave per
                            // segment), 3 piece (K1 + K2, or the speculative S1 + S2), 4 segfuse
 #define WS_SPEC_ADAPT_G 49152
-WsOpt ws_piece_spec{1};    // "piece_spec": 0 never speculative, 1 adaptive (the device's advice from the
-                           // previous call on the slot), 2 speculative whenever the batch fits
+WsOpt ws_piece_spec{0};    // "piece_spec": 0 never speculative (default: with K2 at 6 blocks per CU the
+                           // scan + unmask form is 1.7-2.5 % faster for every frame size measured,
+                           // 16 KiB-256 KiB and cfg4, profiles/r03_spec_sweep.log), 1 adaptive (the
+                           // device's advice from the previous call on the slot), 2 speculative
+                           // whenever the batch fits
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
     if (!strcmp(name, "path")) {
