@@ -270,11 +270,11 @@ def test_state_across_calls_and_shapes(dev):
 
 
 def test_adaptive_choice(dev):
-    """piece_spec 1 (the default): the first call on a stream takes the scan kernel, which
+    """piece_spec 1 (adaptive; the default is 0): the first call on a stream takes the scan kernel, which
     advises the speculative path for a batch of equal frames of >= 48 KiB; a batch of mixed
     lengths makes the repair kernel advise the scan kernel again; equal frames below 48 KiB
     stay on the scan kernel (profiles/r03_spec_sweep.log). Every call bit-exact."""
-    W.set_option("piece_spec", 0)
+    W.set_option("piece_spec", 1)
     W.set_option("spec_g", 0)
     rng = np.random.default_rng(60)
     stream = torch.cuda.Stream(dev)
