@@ -240,3 +240,53 @@ extern "C" __attribute__((visibility("default"))) int exp_batch_touch_k2(
     }
     return 0;
 }
+
+// the raw-stream call once, then `iters` x (the BATCH K1 over the same wire with the batch's
+// own segments and workspace + the stream's K2 on the stream's workspace): does any K1 in
+// front speed up the stream's K2, or only the K1 whose items it reads?
+extern "C" __attribute__((visibility("default"))) int exp_stream_batchk1_k2(
+    unsigned char* buf, unsigned long long len, unsigned int max_frames, WebsocketFrameDesc_t* desc,
+    WebsocketSegResult_t* res, const u64* seg_off, const u64* seg_len, unsigned int nseg, unsigned int fps,
+    WebsocketFrameDesc_t* bdesc, WebsocketSegResult_t* bres, int iters, int with_k1, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    int rc = websocketframeStreamDecodeDevice(buf, len, max_frames, desc, res, hip_stream);
+    if (rc) return rc;
+    const size_t pws = ws_piece_workspace_bytes(len, 1, max_frames);
+    void* ws = nullptr;
+    WsSlot slot;
+    if ((rc = slot.acquire(st)) || (rc = slot.workspace(pws + 64, 16, &ws))) return rc;
+    unsigned char* w8 = reinterpret_cast<unsigned char*>(ws);
+    u64* d_seg = reinterpret_cast<u64*>(w8 + ((pws + 15) & ~(size_t)15));
+    WsLaunch L;
+    L.buf = buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
+    L.desc_base = nullptr; L.desc = desc; L.res = res; L.stream = st;
+    L.cus = slot.cus; L.lds_per_cu = slot.lds;
+    PieceWs Pw;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    Pw.npieces = len + lead0 ? ((len + lead0 - 1) >> WS_PIECE_SHIFT) + 1 : 0;
+    Pw.pbase = 0; Pw.c_lo = 0; Pw.c_hi = (len + lead0 + 15) >> 4;
+    Pw.disorder = reinterpret_cast<u32*>(w8);
+    Pw.nonuni = reinterpret_cast<u32*>(w8) + 1;
+    Pw.ptr = reinterpret_cast<u64*>(w8 + 16);
+    size_t b = (16 + Pw.npieces * 8 + 15) & ~(size_t)15;
+    Pw.nwork = reinterpret_cast<u32*>(w8 + b);
+    b = (b + 4 + 15) & ~(size_t)15;
+    Pw.items = reinterpret_cast<u32x4*>(w8 + b);
+    static unsigned char* bws = nullptr;
+    static size_t bws_bytes = 0;
+    const size_t need = ws_piece_workspace_bytes(len, nseg, fps);
+    if (bws_bytes < need) {
+        if (bws) (void)hipFree(bws);
+        if (hipMalloc(&bws, need) != hipSuccess) return -2;
+        (void)hipMemset(bws, 0, need);
+        bws_bytes = need;
+    }
+    WsLaunch LB = L;
+    LB.seg_off = seg_off; LB.seg_len = seg_len; LB.nseg = nseg; LB.max_frames = fps; LB.desc = bdesc; LB.res = bres;
+    PieceWs PB;
+    for (int i = 0; i < iters; ++i) {
+        if (with_k1 && (rc = ws_launch_piece_scan(LB, 0, len, bws, 99, &PB))) return rc;
+        if ((rc = ws_launch_piece_unmask(L, Pw, 0x7FFFFFF1u))) return rc;
+    }
+    return 0;
+}
