@@ -69,7 +69,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
                                                                 u32x4* __restrict__ items, u32* __restrict__ nwork,
                                                                 u64* __restrict__ ptr, u32* __restrict__ disorder,
                                                                 u32 gen, u64 pbase, u64 lo, u64 hi, u32* nonuni,
-                                                                u32 g0) {
+                                                                u32 g0, WsSegRec* __restrict__ segr) {
     static_assert(G == 16, "group size");
     const u32 lane = threadIdx.x & 63;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
@@ -165,6 +165,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
             if (s == nseg - 1) put_ptrs(ptr, pbase, pend, sorg + sl, hi + lead0, PIECE_NONE);
             ws_store_res(res + s, off, nf, status);
             *gptr<u32>(nwork + s) = cnt;
+            put_item(gptr<u32x4>(reinterpret_cast<u32x4*>(segr + s)), sorg, sorg + sl, cnt);   // WsSegRec
         }
     }
     if (nonuni) {                                                           // one atomic per wave, if any
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
 // exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
 // all measured slower): nontemporal loads and stores, chunks wholly inside
 // segments stored whole (byte coverage by the visited segments), 2^wshift windows.
-template <int NT>
+template <int NT, int SR>
 __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
                                                                   const u64* __restrict__ seg_len, u32 nseg,
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
                                                                   WebsocketSegResult_t* __restrict__ res,
                                                                   u32 wshift, u64 ppw, u64 npieces, u32* nonuni,
-                                                                  int* advice) {
+                                                                  int* advice, const WsSegRec* __restrict__ segr) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
@@ -240,11 +241,25 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     u32 segcov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) segcov[u] = 0;
+    bool first = true;
     while (s < nseg) {
-        const u32 cnt = nwork[s];
+        // the segment: SR = K1's 32-B record (one scalar load), else the caller's tables
+        u64 slo, shi;
+        u32 cnt;
+        if (SR) {
+            const u32x4 R = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(
+                reinterpret_cast<uintptr_t>(segr + s));
+            const u64 w0 = (u64)R.x | ((u64)R.y << 32), w1 = (u64)R.z | ((u64)R.w << 32);
+            slo = w0 & 0xFFFFFFFFFFFFull; shi = w1 & 0xFFFFFFFFFFFFull;
+            cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
+        } else {
+            slo = seg_off[s] + lead0; shi = slo + seg_len[s]; cnt = nwork[s];
+        }
+        if (!first && slo >= r1) break;                                     // the next segment starts past us
+        first = false;
         {
             // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
-            const long long sa = (long long)(seg_off[s] + lead0 - r0), sb = sa + (long long)seg_len[s];
+            const long long sa = (long long)(slo - r0), sb = (long long)(shi - r0);
             const int SA = (int)(sa < -16 ? -16 : (sa > RW + 16 ? RW + 16 : sa));
             const int SB = (int)(sb < -16 ? -16 : (sb > RW + 16 ? RW + 16 : sb));
 #pragma unroll
@@ -291,7 +306,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             if (k + step < cnt) { k += step; step = 64; continue; }         // more items of this segment
         }
         // this segment has no more items: continue with the next one if it starts in range
-        if (++s >= nseg || seg_off[s] + lead0 >= r1) break;
+        ++s;
         k = 0;
         step = 16;
     }
@@ -337,7 +352,8 @@ static u64 piece_count(u64 lo_org, u64 hi_org) {
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     const u64 npieces = (span + 15) / (1ull << PIECE_SHIFT) + 2;
     size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
-    b = (b + (size_t)nseg * 4 + 15) & ~(size_t)15;
+    b = (b + (size_t)nseg * 4 + 31) & ~(size_t)31;
+    b += (size_t)nseg * sizeof(WsSegRec);
     return b + (size_t)nseg * max_frames * 16 + 16;
 }
 
@@ -358,13 +374,15 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     P.ptr = reinterpret_cast<u64*>(ws + 16);
     size_t b = (16 + P.npieces * 8 + 15) & ~(size_t)15;
     P.nwork = reinterpret_cast<u32*>(ws + b);
-    b = (b + (size_t)L.nseg * 4 + 15) & ~(size_t)15;
+    b = (b + (size_t)L.nseg * 4 + 31) & ~(size_t)31;
+    P.segr = reinterpret_cast<WsSegRec*>(ws + b);
+    b += (size_t)L.nseg * sizeof(WsSegRec);
     P.items = reinterpret_cast<u32x4*>(ws + b);
     const u32 blocks = (u32)(((u64)L.nseg * 16 + PSCAN_T - 1) / PSCAN_T);
     hipLaunchKernelGGL(ws_piece_scan_kernel<16>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
                        L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
                        P.disorder, gen, P.pbase, lo, hi, count_nonuniform ? P.nonuni : nullptr,
-                       g0 < (1u << 31) ? g0 : 0u);
+                       g0 < (1u << 31) ? g0 : 0u, P.segr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
     *out = P;
@@ -442,9 +460,16 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
-    hipLaunchKernelGGL(ws_piece_unmask_kernel<1>, dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, L.buf,
-                       L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen, P.pbase,
-                       P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni, advice);
+    if (P.segr)
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
+                           advice, (const WsSegRec*)P.segr);
+    else
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
+                           advice, (const WsSegRec*)nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
     return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
