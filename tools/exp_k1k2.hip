@@ -55,6 +55,17 @@ __global__ __launch_bounds__(256) void exp_read_kernel(const gu32x4* __restrict_
     if (h == 0xA5A5F00Du) *gptr<u32>(sink) = h;
 }
 
+// every CU busy with ALU work (FMA chains) until `ticks` (100 MHz) have passed: no memory traffic
+__global__ __launch_bounds__(256) void exp_alu_kernel(unsigned long long ticks, u32* sink) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) a = __builtin_fmaf(a, b, 1e-7f);
+    }
+    if (a == 12345.f) *gptr<u32>(sink) = 1;
+}
+
 // thread i loads 32 B at base + i*stride + off (clamped to n); the sum never matches the
 // run-time key, so nothing is stored, but the loads cannot be removed
 __global__ __launch_bounds__(256) void exp_touch_kernel(const unsigned char* __restrict__ base, unsigned long long n,
@@ -119,6 +130,9 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
                                reinterpret_cast<const u32*>(buf), buflen / 4, (unsigned long long)(arg % 1000) * 100 * 10,
                                sink);
             break;
+        case 16: case 17:                       // the whole GPU ALU-busy for arg us (+ K2 for 16)
+            hipLaunchKernelGGL(exp_alu_kernel, dim3(2048), dim3(256), 0, st, (unsigned long long)arg * 100, sink);
+            break;
         case 13:                                // K1, then a plain XOR of arg MiB of `other`, then K2
             if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
             hipLaunchKernelGGL(exp_xor_kernel, dim3(4096), dim3(256), 0, st,
@@ -137,7 +151,7 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
         default: break;
         }
-        if ((mode <= 5 || mode == 9 || mode == 11 || mode >= 13) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16)) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
