@@ -221,7 +221,8 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
  * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream: chunk-parallel
- * walk, log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
+ * walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront; log2 of its
+ * largest chunk 16..26, pass rounds of a captured call 1..64, a captured
  * call's chunk records linked in parallel 0/1), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */

@@ -26,7 +26,7 @@ DEFAULTS = {"path": -1, "piece_spec": 0, "spec_g": 0, "spec_spins": 2048, "host_
 VALUES = {"path": [-1, 1, 3, 4], "piece_spec": [0, 1, 2], "spec_g": [0, 2, 1030, 16384], "spec_spins": [0, 1, 2048],
           "host_chunk_mb": [1, 64], "piece_lds": [0, 1, 56000], "piece_win": [0, 1, 2, 3, 4, 5, 6],
           "seg_win": [0, 1], "reasm_path": [0, 1, 2], "reasm_cfg": [0, 1, 2], "enc_front": [0, 1],
-          "stream_rw": [0, 1], "stream_rw_cmax": [16, 20, 23, 26], "stream_rounds": [1, 4, 64], "stream_plink": [0, 1],
+          "stream_rw": [0, 1, 2], "stream_rw_cmax": [16, 20, 23, 26], "stream_rounds": [1, 4, 64], "stream_plink": [0, 1],
           "k2_timing": [0, 1]}
 
 # options that act only inside the piece path: the case runs it (speculative for the spec_* knobs)

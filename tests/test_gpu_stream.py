@@ -116,7 +116,11 @@ def serial_walk():
 def test_long_stream_cfg3_mix(dev, shift):
     """the cfg3 length mix as one 48 MiB client stream (16 MiB chunks)"""
     wire = long_stream(np.random.default_rng(21), 48 << 20, mix3, masked=1.0)
-    r = run(dev, wire, 1 << 16, shift)
+    W.set_option("stream_rw", 2)                  # the host follows the records: its counters
+    try:
+        r = run(dev, wire, 1 << 16, shift)
+    finally:
+        W.set_option("stream_rw", 1)
     assert int(r["consumed"]) == len(wire) and int(r["status"]) == W.SEG_OK
     # every chunk from the speculative records (no one-wavefront chunk walks; an unmasked
     # frame in a client stream would end its chunk's speculation)

@@ -100,7 +100,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_enc_front = (int)value;
     }
     else if (!strcmp(name, "stream_rw")) {
-        if (value < 0 || value > 1) return -1;
+        if (value < 0 || value > 2) return -1;
         ws_stream_rw = (int)value;
     }
     else if (!strcmp(name, "stream_rw_cmax")) {

@@ -1067,7 +1067,8 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     if (lane == 0) plan->nrows = rows;
 }
 
-WsOpt ws_stream_rw{1};          // "stream_rw": 1 chunk-parallel walk for long streams, 0 one wavefront
+WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long streams, linked on the device
+                                // (1) or by the host (2, eager calls), 0 one wavefront
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
@@ -1356,14 +1357,18 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     // round while rounds pay, the chunk-parallel walk once lengths keep changing. A captured
     // call (and any shorter stream) never reads it: `nr` rounds, the last one's resolve also
     // walks whatever is left with one wavefront.
-    const bool rw = ws_stream_rw != 0;
+    const int rw_opt = ws_stream_rw;                                         // one read per call
+    const bool rw = rw_opt != 0;
     const bool host_rw = rw && len >= RW_MIN && !capture;
     // a captured call on a long stream runs the chunk-parallel walk on the device (its
-    // scratch, sized from the length, follows the state in the aux workspace)
+    // scratch, sized from the length, follows the state in the aux workspace); so does an
+    // eager call once its published state says the lengths keep changing (stream_rw 1), unless
+    // stream_rw 2 asks for the host to follow the chunk records (round 2's eager form)
     const bool dev_rw = rw && len >= RW_MIN && capture;
-    const RwDevLayout RL = dev_rw ? rw_dev_layout(len) : RwDevLayout{};
+    const bool dev_layout = rw && len >= RW_MIN && (capture || rw_opt == 1);
+    const RwDevLayout RL = dev_layout ? rw_dev_layout(len) : RwDevLayout{};
     WsAux A;
-    if ((rc = slot.aux(WS_AUX_HEAD + (dev_rw ? RL.bytes : 0), host_rw ? WS_AUX_HEAD : 0, &A))) return rc;
+    if ((rc = slot.aux(WS_AUX_HEAD + (dev_layout ? RL.bytes : 0), host_rw ? WS_AUX_HEAD : 0, &A))) return rc;
     SdState* sd = reinterpret_cast<SdState*>(A.d);
     SdMirror* hm = host_rw ? reinterpret_cast<SdMirror*>(A.h) : nullptr;
     SdMirror* dm = host_rw ? reinterpret_cast<SdMirror*>(A.h_dev) : nullptr;
@@ -1449,7 +1454,11 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     if (hm->phase != SD_DONE) {
         const u64 P = hm->P;
         const u32 nf = hm->nf;
-        if (len - P >= RW_MIN) {                                             // lengths keep changing
+        if (len - P >= RW_MIN && rw_opt == 1) {                              // lengths keep changing:
+            if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,    // the device walks
+                                     reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL)))
+                return rc;
+        } else if (len - P >= RW_MIN) {                                      // ... the host follows
             if ((rc = rw_walk(slot, d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
         } else {
             hipLaunchKernelGGL(ws_stream_finish_kernel, dim3(1), dim3(64), 0, st, d_buf, (u64)len, max_frames, d_desc,
