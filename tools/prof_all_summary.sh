@@ -11,5 +11,5 @@ S segfuse_cfg5 ws_segfuse_kernel
 S reasm_fused ws_reasm_seg_kernel
 S encode_cfg2 ws_enc_copy_kernel,ws_enc_front_kernel,ws_enc_tsum_kernel,ws_enc_tscan_kernel,ws_enc_edge_kernel,ws_enc_ptr_kernel
 S stream_cfg2 $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel
-S stream_cfg3 $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel,ws_rw_own_kernel,ws_rw_cand_kernel,ws_rw_spec_kernel,ws_rw_emit_kernel,ws_rw_chunk_kernel,ws_stream_finish_kernel
+S stream_cfg3 $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel,ws_rw_plan_kernel,ws_rw_own_kernel,ws_rw_cand_kernel,ws_rw_spec_kernel,ws_rw_plink_kernel,ws_rw_pscan_kernel,ws_rw_link_kernel,ws_rw_emit_kernel,ws_rw_chunk_kernel,ws_stream_finish_kernel
 S stream_cfg3_graph $K2,ws_stream_pass_kernel,ws_stream_resolve_kernel,ws_rw_plan_kernel,ws_rw_own_kernel,ws_rw_cand_kernel,ws_rw_spec_kernel,ws_rw_plink_kernel,ws_rw_pscan_kernel,ws_rw_link_kernel,ws_rw_emit_kernel
