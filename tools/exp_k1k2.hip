@@ -133,6 +133,11 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
         case 16: case 17:                       // the whole GPU ALU-busy for arg us (+ K2 for 16)
             hipLaunchKernelGGL(exp_alu_kernel, dim3(2048), dim3(256), 0, st, (unsigned long long)arg * 100, sink);
             break;
+        case 18: case 19:                       // a plain XOR of arg MiB of `other` (+ K2 for 18)
+            hipLaunchKernelGGL(exp_xor_kernel, dim3(4096), dim3(256), 0, st,
+                               reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(other)),
+                               (unsigned long long)arg << 16);
+            break;
         case 13:                                // K1, then a plain XOR of arg MiB of `other`, then K2
             if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
             hipLaunchKernelGGL(exp_xor_kernel, dim3(4096), dim3(256), 0, st,
@@ -151,7 +156,7 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
         default: break;
         }
-        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16)) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16) || mode == 18) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
