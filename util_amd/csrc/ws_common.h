@@ -40,9 +40,12 @@ __device__ __forceinline__ u32x4 ld16(const gu32x4* p) {
     if constexpr (NT == 1) return __builtin_nontemporal_load(p);
     else return *p;
 }
+#ifndef WS_ST16_PLAIN
+#define WS_ST16_PLAIN 0   // (A/B builds: 1 = every st16 a plain store)
+#endif
 template <int NT>
 __device__ __forceinline__ void st16(u32x4 v, gu32x4* p) {
-    if constexpr (NT >= 1) __builtin_nontemporal_store(v, p);
+    if constexpr (NT >= 1 && !WS_ST16_PLAIN) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
