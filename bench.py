@@ -33,12 +33,10 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel that dominates the step, per websocketframeGpuSetOption("path") value
-KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel", 5: "ws_piece_spec_kernel"}
+KERNELS = {1: "ws_walker_kernel", 3: "ws_piece_unmask_kernel", 4: "ws_segfuse_kernel"}
 STEP_KERNELS = {3: "ws_piece_scan_kernel<16> + ws_piece_unmask_kernel (which decodes unordered batches itself, "
                    "one wave per segment)",
-                4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)",
-                5: "ws_piece_spec_kernel (speculative frame grid, verified in the unmask) + ws_piece_spec_fix_kernel "
-                   "(repair of mispredicted segments; exits at once when there are none)"}
+                4: "ws_segfuse_kernel (one launch: walk + unmask, one workgroup per rx segment)"}
 DEFAULT_PATH = -1  # auto: 4 (segfuse) for >= 1024 segments of <= 17 KiB - 64 B average, max_frames <= 64; else 3
 
 
@@ -827,27 +825,52 @@ def free_port():
         return sk.getsockname()[1]
 
 
-def launch_ranks(n):
+def launch_ranks(n, poll_s=0.1, grace_s=10.0):
     """`python bench.py --gpus N` without a launcher: start N ranks of this same command as
     child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, one GPU
     each; WS_BENCH_RANKS_PER_GPU > 1 packs ranks onto fewer GPUs for rehearsal), relay rank 0's
-    JSON line, and return non-zero if any rank failed. This process never touches a GPU."""
+    JSON line, and return non-zero if any rank failed. Every rank is polled: as soon as one
+    exits non-zero the others are terminated (they would otherwise block in a rendezvous or a
+    collective until torch.distributed's timeout). This process never touches a GPU."""
     import subprocess
+    import tempfile
+    import time
     port = str(free_port())
     procs = []
+    out_f = tempfile.TemporaryFile()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate()[0]
-    rcs = [p.wait() for p in procs]
-    if out:
+                                      stdout=out_f if r == 0 else subprocess.DEVNULL))
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        failed = next((r for r, p in enumerate(procs) if p.poll() not in (None, 0)), None)
+        if failed is None:
+            time.sleep(poll_s)
+    if failed is None:
+        failed = next((r for r, p in enumerate(procs) if p.returncode), None)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    rcs = [p.returncode for p in procs]
+    out_f.seek(0)
+    out = out_f.read()
+    out_f.close()
+    if out and failed is None:
         _RESULT_OUT.write(out.decode())
         _RESULT_OUT.flush()
     bad = [(r, rc) for r, rc in enumerate(rcs) if rc]
     if bad:
-        sys.stderr.write("bench.py: ranks failed: %s\n" % bad)
+        sys.stderr.write("bench.py: ranks failed: %s (first: rank %s)\n" % (bad, failed))
     return 1 if bad or not out else 0
 
 
@@ -898,6 +921,9 @@ def main():
     elif os.environ.get("WS_BENCH_LAUNCH_ECHO"):                   # launcher test (tests/test_dist.py)
         emit({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
               "local_rank": int(os.environ["LOCAL_RANK"]), "master_port": os.environ["MASTER_PORT"]})
+        if os.environ["RANK"] == "0" and os.environ.get("WS_BENCH_LAUNCH_ECHO_HANG"):
+            import time                                            # a rank stuck in a rendezvous
+            time.sleep(float(os.environ["WS_BENCH_LAUNCH_ECHO_HANG"]))
         sys.exit(int(os.environ.get("WS_BENCH_LAUNCH_ECHO_RC", "0")) if os.environ["RANK"] != "0" else 0)
     elif int(os.environ["WORLD_SIZE"]) != args.gpus:
         sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%s: refusing to report a %s-rank run as %d GPUs\n"
@@ -977,9 +1003,7 @@ def main():
         def step():
             graph.replay()
             wl.decodes += 1
-    spec0 = wl.W.get_stat("piece_spec_calls")
     elapsed, step_ms = timed_region(step, args.steps, world)
-    spec_steps = wl.W.get_stat("piece_spec_calls") - spec0          # path 3: calls that took the speculative form
     kern_ms = np.array([step_ms])
     from util_amd import dist as D
     elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
@@ -989,10 +1013,8 @@ def main():
     # k2_timing), over a second region of the same calls (events between kernels would
     # perturb the contract's region above, so it is not timed this way)
     kpath = decode_path(path, wl)
-    if kpath == 3 and spec_steps == args.steps:
-        kpath = 5                                                   # every timed call was speculative
     k2_ms = None
-    if kpath in (3, 5) and not args.graph:
+    if kpath == 3 and not args.graph:
         wl.W.set_option("k2_timing", 1)
         for _ in range(args.steps):
             wl.decode()

@@ -208,13 +208,8 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
  * configuration; every value yields bit-identical results, each one is parity-tested in
- * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_spec"
- * (path 3: 0 always the scan kernel + unmask (default), 1 adaptive — speculative, with no scan kernel,
- * when the previous eager call on the stream advised it — 2 speculative whenever the batch
- * fits), "spec_spins" (the speculative kernel's bounded wait for its table checkers; 0 gives
- * up at once, exercising its repair path), "spec_g" (0: the speculative kernel predicts
- * frames of the length the previous call on the stream saw first; >= 2 forces that length,
- * for tests of mispredictions), "piece_lds" (unused dynamic LDS per unmask block:
+ * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_lds"
+ * (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
@@ -228,8 +223,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
-/* Counters (diagnostics): "piece_spec_calls" / "piece_classic_calls" (path-3 calls that took
- * the speculative / the scan + unmask form, since load), "workspace_bytes" (device bytes held
+/* Counters (diagnostics): "workspace_bytes" (device bytes held
  * in workspace slots), and of the calling process's most recent call: "stream_rw_chunks"
  * (chunks of a long stream written from the chunk-parallel walk's records),
  * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront); with the option

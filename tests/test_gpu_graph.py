@@ -250,3 +250,51 @@ def test_capture_workspaces_released_with_their_graphs(dev, kind):
         del g
     after = settle()
     assert after <= one, (one, after)
+
+
+@pytest.mark.parametrize("kind", ["batch", "stream"])
+def test_capture_only_process_reuses_dead_slots(dev, kind):
+    """a process that only captures, replays and destroys graphs (no eager library call frees the
+    slots of destroyed graphs): each new capture adopts a dead graph's idle slot, so 30 such
+    cycles hold no more device workspace than the first two, and every adopted slot's replay
+    is still bit-exact vs the oracle"""
+    import gc
+    import time
+    rng = np.random.default_rng(44)
+    wire, so, sl = random_stream(rng, 200)
+    n = len(wire)
+    ob = wire.copy()
+    if kind == "batch":
+        od, orr = oracle_segments(ob, so, sl, 16)
+    else:
+        od, orr = oracle_segments(ob, [0], [n], n // 2 + 1)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    so_t = torch.tensor(so, dtype=torch.int64, device=dev)
+    sl_t = torch.tensor(sl, dtype=torch.int64, device=dev)
+    desc = torch.zeros(max(len(so), n // 2 + 1) * 16 * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(wire).to(dev)
+
+    def cycle():
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            if kind == "batch":
+                W.batch_decode_device(d, so_t, sl_t, 16, desc, res)
+            else:
+                W.stream_decode_device(d, n, n // 2 + 1, desc, res)
+        d[:n].copy_(src)
+        g.replay()
+        torch.cuda.synchronize()
+        out = d[:n].cpu().numpy()
+        assert np.array_equal(out, ob)
+        del g
+        for _ in range(3):
+            gc.collect()
+            time.sleep(0.01)
+
+    cycle()
+    cycle()
+    base = W.get_stat("workspace_bytes")
+    for _ in range(30):
+        cycle()
+    assert W.get_stat("workspace_bytes") <= base, (base, W.get_stat("workspace_bytes"))

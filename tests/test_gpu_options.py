@@ -2,7 +2,7 @@
 (include/wsframe_amd.h) gives results bit-identical to the oracle: one matrix case per
 (option, value), each running the same small workloads through the decode (irregular and
 uniform batches), raw stream, reassembly and encode entry points. The focused tests of each
-option (test_gpu_spec.py, test_gpu_stream.py, test_gpu_reasm.py, test_gpu_encode.py,
+option (test_gpu_stream.py, test_gpu_reasm.py, test_gpu_encode.py,
 test_gpu_parity.py::test_window_mappings) cover the shapes where a value changes the launch."""
 import numpy as np
 import pytest
@@ -19,19 +19,18 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-DEFAULTS = {"path": -1, "piece_spec": 0, "spec_g": 0, "spec_spins": 2048, "host_chunk_mb": 64, "piece_lds": 0,
+DEFAULTS = {"path": -1, "host_chunk_mb": 64, "piece_lds": 0,
             "piece_win": 1, "seg_win": 1, "reasm_path": 0, "reasm_cfg": 0, "enc_front": 1, "stream_rw": 1,
             "stream_rw_cmax": 23, "stream_rounds": 4, "stream_plink": 1, "k2_timing": 0}
 
-VALUES = {"path": [-1, 1, 3, 4], "piece_spec": [0, 1, 2], "spec_g": [0, 2, 1030, 16384], "spec_spins": [0, 1, 2048],
+VALUES = {"path": [-1, 1, 3, 4],
           "host_chunk_mb": [1, 64], "piece_lds": [0, 1, 56000], "piece_win": [0, 1, 2, 3, 4, 5, 6],
           "seg_win": [0, 1], "reasm_path": [0, 1, 2], "reasm_cfg": [0, 1, 2], "enc_front": [0, 1],
           "stream_rw": [0, 1, 2], "stream_rw_cmax": [16, 20, 23, 26], "stream_rounds": [1, 4, 64], "stream_plink": [0, 1],
           "k2_timing": [0, 1]}
 
-# options that act only inside the piece path: the case runs it (speculative for the spec_* knobs)
-CONTEXT = {"piece_spec": {"path": 3}, "spec_g": {"path": 3, "piece_spec": 2},
-           "spec_spins": {"path": 3, "piece_spec": 2}, "piece_lds": {"path": 3}, "piece_win": {"path": 3}}
+# options that act only inside the piece path: the case runs it
+CONTEXT = {"piece_lds": {"path": 3}, "piece_win": {"path": 3}}
 
 CASES = [(o, v) for o, vals in VALUES.items() for v in vals]
 
@@ -93,16 +92,14 @@ def test_option_value_parity(dev, work, opt, val):
         assert np.array_equal(out[:len(want)], np.frombuffer(want, dtype=np.uint8)), tag
         if opt == "k2_timing" and val:
             assert W.get_stat("k2_calls") > 0
-        if opt == "piece_spec" and val == 2:
-            assert W.get_stat("piece_spec_calls") > 0
     finally:
         for k in set(ctx) | {opt}:
             W.set_option(k, DEFAULTS[k])
 
 
 def test_out_of_range_values_refused():
-    for opt, bad in [("path", 2), ("piece_spec", 3), ("spec_g", 1), ("piece_win", 7), ("seg_win", 2),
+    for opt, bad in [("path", 2), ("piece_win", 7), ("seg_win", 2),
                      ("reasm_path", 3), ("reasm_cfg", 3), ("enc_front", 2), ("stream_rw_cmax", 27),
-                     ("stream_rounds", 0), ("host_chunk_mb", 0), ("piece_lds", -1), ("spec_spins", -1)]:
+                     ("stream_rounds", 0), ("host_chunk_mb", 0), ("piece_lds", -1)]:
         with pytest.raises(ValueError):
             W.set_option(opt, bad)

@@ -25,18 +25,13 @@ def dev():
     return torch.device("cuda:0")
 
 
-# decode variants: -1 auto (the default: 4 for many small segments, else 3; path 3 takes the
-# speculative form when the previous call on the stream advised it), 3 the classic piece path
-# (scan kernel + one-shot 16 KiB piece unmask), 5 = path 3 forced speculative (no scan kernel,
-# ws_spec.hip), 4 one workgroup per segment (segfuse)
-@pytest.fixture(params=[(-1, 0), (3, 1), (3, 2), (4, 0)], ids=["auto", "piece", "spec", "segfuse"], autouse=True)
+# decode variants: -1 auto (the default: 4 for many small segments, else 3), 3 the piece path
+# (scan kernel + one-shot 16 KiB piece unmask), 4 one workgroup per segment (segfuse)
+@pytest.fixture(params=[-1, 3, 4], ids=["auto", "piece", "segfuse"], autouse=True)
 def decode_path(request):
-    path, spec = request.param
-    W.set_option("path", path)
-    W.set_option("piece_spec", spec)
-    yield 5 if spec == 2 else path
+    W.set_option("path", request.param)
+    yield request.param
     W.set_option("path", -1)
-    W.set_option("piece_spec", 0)
 
 
 def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):
@@ -439,3 +434,51 @@ def test_host_path_never_writes_between_segments(dev, decode_path):
     assert np.array_equal(buf[:a], plain[:a]) and np.array_equal(buf[2 * page:2 * page + len(wire) - a], plain[a:])
     assert (buf[page:2 * page] == 0xA5).all()
     del buf
+
+
+def _segments_of(off, n, fps, total):
+    so = [int(off[i]) for i in range(0, n, fps)]
+    ends = so[1:] + [total]
+    return so, [e - s for s, e in zip(so, ends)]
+
+
+def test_stride_hint_never_changes_results(dev, decode_path):
+    """K1's first step guesses the stride from the previous call's first frame length (the
+    device's hint, eager calls on one stream). Every batch below follows a uniform batch of
+    another frame length, or of the same first length with other lengths after it, or with
+    bytes at the guessed stride that parse as frames of the guessed length: each decode is
+    bit-exact vs the oracle whatever the hint was"""
+    if decode_path != 3:
+        pytest.skip("the hint is the piece path's")
+    primer = {}
+    for plen in (4096, 1000, 125):
+        wire, off, pl, plain = wsynth.make_batch(64, wsynth.PLEN_FIXED, plen, wsynth.B0_BINARY, 90 + plen)
+        primer[plen] = (wire, *_segments_of(off, 64, 16, len(wire)))
+    # a 4104-B first frame, then 1008-B frames whose payload holds fake 4104-B headers at every
+    # multiple of 4104 from the segment start (the positions the guessed stride parses)
+    fake = wsynth.header(0x82, 4096, 0x01020304)
+    segs = []
+    for s in range(8):
+        frames = [wsynth.header(0x82, 4096, 0xA0B0C0D0 + s), np.full(4096, s, np.uint8)]
+        body = np.random.default_rng(s).integers(0, 256, 20 * 1000, dtype=np.uint8)
+        pos = 4104
+        for k in range(20):
+            frames.append(wsynth.header(0x82, 1000, 0x11223344 * (k + 1) & 0xFFFFFFFF))
+            frames.append(body[1000 * k:1000 * (k + 1)].copy())
+        seg = np.concatenate(frames)
+        for m in range(2, len(seg) // 4104):
+            p = m * 4104
+            if p + len(fake) <= len(seg):
+                seg[p:p + len(fake)] = fake
+        segs.append(seg)
+    crafted = np.concatenate(segs)
+    so = list(np.cumsum([0] + [len(x) for x in segs[:-1]]))
+    crafted_case = (crafted, [int(x) for x in so], [len(x) for x in segs])
+    mixed, off, pl, plain = wsynth.make_batch(96, wsynth.PLEN_MIX3, 0, wsynth.B0_BINARY, 5)
+    mixed_case = (mixed, *_segments_of(off, 96, 16, len(mixed)))
+    for first, then in [(4096, primer[1000]), (1000, primer[4096]), (4096, crafted_case), (125, crafted_case),
+                        (4096, mixed_case), (125, primer[4096])]:
+        pw, pso, psl = primer[first]
+        gpu_decode(dev, pw.copy(), pso, psl, 64)          # sets the hint for the next call on the stream
+        wire, so2, sl2 = then
+        assert_same(dev, wire, so2, sl2, 64, tag="hint %d" % first)

@@ -4,5 +4,5 @@ cd "$(dirname "$0")/.."
 make -C util_amd/csrc -s
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c tools/exp_k1k2.hip -o build/obj/exp_k1k2.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC build/obj/ws_host.o build/obj/ws_channel.o build/obj/ws_api.o \
-  build/obj/ws_hostpath.o build/obj/ws_segfuse.o build/obj/ws_piece.o build/obj/ws_spec.o build/obj/ws_stream.o \
+  build/obj/ws_hostpath.o build/obj/ws_segfuse.o build/obj/ws_piece.o build/obj/ws_stream.o \
   build/obj/ws_reasm.o build/obj/ws_encode.o build/obj/ws_walker.o build/obj/exp_k1k2.o -o tools/libexp_k1k2.so

@@ -30,8 +30,6 @@ extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
-extern WsOpt ws_spec_spins;
-WsOpt ws_spec_g{0};        // "spec_g": the frame length the speculative path predicts with (0: the device's hint)
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
@@ -54,22 +52,12 @@ extern "C" WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void) { ret
 // parity-tested, tests/test_gpu_options.py)
 
 static WsOpt g_path{-1};   // "path": -1 auto (4 for many small segments, else 3), 1 walker (one wave per
-                           // segment), 3 piece (K1 + K2, or the speculative S1 + S2), 4 segfuse
-#define WS_SPEC_ADAPT_G 49152
-WsOpt ws_piece_spec{0};    // "piece_spec": 0 never speculative (default: with K2 at 6 blocks per CU the
-                           // scan + unmask form is 1.7-2.5 % faster for every frame size measured,
-                           // 16 KiB-256 KiB and cfg4, profiles/r03_spec_sweep.log), 1 adaptive (the
-                           // device's advice from the previous call on the slot), 2 speculative
-                           // whenever the batch fits
+                           // segment), 3 piece (K1 + K2), 4 segfuse
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value) {
     if (!strcmp(name, "path")) {
         if (value != -1 && value != 1 && value != 3 && value != 4) return -1;
         g_path = (int)value;
-    }
-    else if (!strcmp(name, "piece_spec")) {
-        if (value < 0 || value > 2) return -1;
-        ws_piece_spec = (int)value;
     }
     else if (!strcmp(name, "host_chunk_mb")) {
         if (value <= 0 || value > 65536) return -1;
@@ -115,14 +103,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
     }
-    else if (!strcmp(name, "spec_g")) {
-        if (value < 0 || value >= (1ll << 31) || value == 1) return -1;
-        ws_spec_g = (int)value;
-    }
-    else if (!strcmp(name, "spec_spins")) {
-        if (value < 0 || value > (1 << 20)) return -1;
-        ws_spec_spins = (int)value;
-    }
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = value ? 1 : 0;
         ws_k2_timing_reset();
@@ -130,8 +110,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else return -1;
     return 0;
 }
-
-extern std::atomic<unsigned long long> ws_stat_spec_calls, ws_stat_classic_calls;
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, unsigned long long* value) {
     if (!value) return -1;
@@ -143,8 +121,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     }
     if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks.load();
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
-    else if (!strcmp(name, "piece_spec_calls")) *value = ws_stat_spec_calls.load();
-    else if (!strcmp(name, "piece_classic_calls")) *value = ws_stat_classic_calls.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
     else return -1;
     return 0;
@@ -157,7 +133,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
 // by the stream. A call pins its slot for its whole duration (WsSlot): LRU eviction never
 // takes a pinned slot. A graph capture's slot belongs to that graph: a HIP user object on the
 // graph marks it dead when the graph (and every executable made from it) is destroyed, and the
-// next eager library call frees its buffers.
+// next eager library call frees its buffers (or the next capture adopts them, slot_rezero).
 #define WS_MAX_DEV 64
 #define WS_STREAM_SLOTS 16
 struct WsStreamWs {
@@ -178,12 +154,7 @@ struct WsStreamWs {
     void* hws_dev = nullptr;       // (its device address)
     size_t hws_bytes = 0;
     bool aux_state_ok = false;     // the stream path's state (aux head) rests at zero
-    unsigned char* sws = nullptr;  // speculative piece path state (ws_spec.hip)
-    size_t sws_bytes = 0;
-    u32 spec_zero_nseg = 0;        // flags [0, this) rest at zero
-    u32 spec_parity = 0, spec_tag = 0;
-    bool spec_dirty = false;       // a call stopped between its two launches: heads not reset
-    int* adv_h = nullptr;          // pinned host word: the device's advice for the next path choice
+    int* adv_h = nullptr;          // pinned host words: the device's stride hint for the next call
     int* adv_d = nullptr;
     std::vector<void*> retired;    // buffers replaced while capturing (the graph still uses them)
 };
@@ -196,13 +167,12 @@ struct WsDevState {
 };
 static WsDevState g_dev[WS_MAX_DEV];
 static std::mutex g_dev_mu;        // device init and the stream-slot table
-std::atomic<unsigned long long> ws_stat_spec_calls{0}, ws_stat_classic_calls{0};
 
 size_t ws_workspace_bytes_total() {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     size_t t = 0;
     for (auto& d : g_dev)
-        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes + w.sws_bytes;
+        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes;
     return t;
 }
 
@@ -243,18 +213,14 @@ static void slot_free(WsStreamWs& w) {
     (void)hipFree(w.ws);
     (void)hipFree(w.ews);
     (void)hipFree(w.aws);
-    (void)hipFree(w.sws);
     if (w.hws) (void)hipHostFree(w.hws);
     if (w.adv_h) (void)hipHostFree(w.adv_h);
     for (void* p : w.retired) (void)hipFree(p);
     w.retired.clear();
-    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.sws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
+    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
     w.adv_h = nullptr; w.adv_d = nullptr;
-    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.sws_bytes = w.hws_bytes = 0;
+    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = 0;
     w.aux_state_ok = false;
-    w.spec_zero_nseg = 0;
-    w.spec_parity = 0;
-    w.spec_dirty = false;
     w.stream = nullptr;
     w.capture = 0;
     w.used = false;
@@ -263,6 +229,24 @@ static void slot_free(WsStreamWs& w) {
 }
 
 static void capture_slot_destroyed(void* p) { reinterpret_cast<WsStreamWs*>(p)->dead.store(1); }
+
+// zero the resting heads of a slot's buffers (decode/reassembly/stream workspace: 16 B; the
+// auxiliary scratch: WS_AUX_HEAD) outside any capture: private stream, relaxed capture mode
+static int slot_rezero(WsStreamWs& w) {
+    if (!w.ws && !w.aws) return 0;
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+    hipStream_t ps = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+    if (e == hipSuccess && w.ws) e = hipMemsetAsync(w.ws, 0, 16, ps);
+    if (e == hipSuccess && w.aws) e = hipMemsetAsync(w.aws, 0, WS_AUX_HEAD, ps);
+    if (e == hipSuccess) e = hipStreamSynchronize(ps);
+    if (ps) (void)hipStreamDestroy(ps);
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+    if (e != hipSuccess) return ws_set_err("workspace re-zero (adopted capture slot)", e);
+    if (w.aws) w.aux_state_ok = true;
+    return 0;
+}
 
 // the slot of (stream, capture) (caller holds g_dev_mu), pinned. Eager calls keep at most
 // WS_STREAM_SLOTS slots: a further stream takes the least recently used idle one after a
@@ -290,6 +274,7 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
     }
     WsStreamWs* lru = nullptr;
     WsStreamWs* freeslot = nullptr;
+    WsStreamWs* adopt = nullptr;   // a destroyed graph's idle slot: a new capture takes its buffers
     size_t eager = 0;
     for (WsStreamWs& w : ds->sw) {
         if (w.used && w.stream == stream && w.capture == cap && !w.dead.load()) {
@@ -302,13 +287,25 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
             if (!freeslot) freeslot = &w;
             continue;
         }
+        if (w.captured && w.dead.load() && !w.busy) {
+            if (!adopt) adopt = &w;
+            continue;
+        }
         if (!w.captured) {
             ++eager;
             if (!w.busy && (!lru || w.last < lru->last)) lru = &w;
         }
     }
     WsStreamWs* w = nullptr;
-    if (freeslot) {
+    if (cap && adopt) {
+        // a process that only captures, replays and destroys graphs never makes the eager call that
+        // frees dead slots: the new capture reuses one as it is (no hipFree inside a capture), with
+        // the workspace heads zeroed once on a private stream, as a fresh allocation would be
+        int rc = slot_rezero(*adopt);
+        if (rc) return rc;
+        w = adopt;
+        w->dead = 0;
+    } else if (freeslot) {
         w = freeslot;
     } else if (cap || eager < WS_STREAM_SLOTS || !lru) {
         ds->sw.emplace_back();
@@ -330,7 +327,12 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
         hipError_t e = hipUserObjectCreate(&uo, w, capture_slot_destroyed, 1, hipUserObjectNoDestructorSync);
         if (e == hipSuccess) e = hipGraphRetainUserObject(graph, uo, 1, hipGraphUserObjectMove);
         if (e != hipSuccess) {
+            // the slot is not tied to any graph: hand it back (its buffers stay for the next user)
             --w->busy;
+            w->used = false;
+            w->captured = false;
+            w->capture = 0;
+            w->stream = nullptr;
             return ws_set_err("hipUserObjectCreate (capture workspace)", e);
         }
     }
@@ -454,7 +456,8 @@ int WsSlot::aux(size_t dbytes, size_t hbytes, WsAux* out) {
     return 0;
 }
 
-// the pinned advice word (eager calls only): 1 = the last call says take the speculative path
+// the pinned advice words (eager calls only): [0] 1 = nearly every segment of the last call held frames of
+// one length, [1] the length of its first frame (K1's first-step stride guess for the next call)
 int WsSlot::advice(int** host, int** dev) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     if (!w->adv_h) {
@@ -468,40 +471,6 @@ int WsSlot::advice(int** host, int** dev) {
     *host = w->adv_h;
     *dev = w->adv_d;
     return 0;
-}
-
-// the speculative path's state for a call over nseg segments of a span-byte range: heads +
-// flags at rest (zeroed here when needed), this call's head parity and range tag
-int WsSlot::spec(u64 span, u32 nseg, unsigned char** sws, u32* parity, u32* tag) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    const size_t need = ws_spec_workspace_bytes(span, nseg);
-    void* p = w->sws;
-    const size_t had = w->sws_bytes;
-    int rc = grow(w, &p, &w->sws_bytes, need, st, ws_spec_zero_bytes(nseg), "hipMalloc(spec workspace)");
-    w->sws = reinterpret_cast<unsigned char*>(p);
-    if (rc) return rc;
-    hipError_t e;
-    if (w->sws_bytes != had) {
-        w->spec_zero_nseg = nseg;                                   // fresh: heads + flags zeroed
-        w->spec_dirty = false;
-    }
-    if (w->spec_dirty && (e = hipMemsetAsync(w->sws, 0, ws_spec_flags_off(), st)) != hipSuccess)
-        return ws_set_err("spec reset", e);
-    w->spec_dirty = false;
-    if (nseg > w->spec_zero_nseg &&
-        (e = hipMemsetAsync(w->sws + ws_spec_flags_off(), 0, (size_t)nseg * 4, st)) != hipSuccess)
-        return ws_set_err("spec flags reset", e);
-    w->spec_zero_nseg = nseg;           // flags past nseg may be overwritten by this call's list
-    *sws = w->sws;
-    *parity = w->spec_parity++;
-    w->spec_tag = (w->spec_tag + 1) & 0x7FFFFFFFu;
-    *tag = 0x80000000u | w->spec_tag;   // never a segment index (the list region) or a flag value
-    return 0;
-}
-
-void WsSlot::spec_failed() {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    w->spec_dirty = true;
 }
 
 bool ws_capturing(hipStream_t stream) { return capturing(stream); }
@@ -553,31 +522,10 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     int* adv_d = nullptr;
     if (!ws) {
         if ((rc = slot.acquire(stream))) return rc;
-        const bool cap = capturing(stream);
-        const int spec_opt = ws_piece_spec;
-        if (!cap && (rc = slot.advice(&adv_h, &adv_d))) return rc;
-        // speculative (no K1): eager calls only, when the checkers can cover the segment table,
-        // and, adaptive, when the device advised it after the previous call on this slot and
-        // that call's first frame was >= WS_SPEC_ADAPT_G bytes (below that the classic form is
-        // as fast or faster: K1 costs little there, and K2 right behind K1 streams faster than
-        // any one-pass kernel, profiles/r03_spec_sweep.log); forced: whenever it fits
-        // (the device's advice and frame-length hint: adv_h[0], adv_h[1]; option spec_g overrides the hint)
-        // (captured calls have no advice word and never speculate)
-        int hint = ws_spec_g > 0 ? (int)ws_spec_g : adv_h ? __atomic_load_n(adv_h + 1, __ATOMIC_RELAXED) : 0;
-        if (spec_opt == 2 && hint < 2) hint = 1024;     // forced with no hint yet: any length verifies
-        if (!cap && spec_opt && hint >= 2 && hint < (1 << 30) && ws_spec_fits(hi - lo, nseg) &&
-            (spec_opt == 2 || (__atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1 && hint >= WS_SPEC_ADAPT_G))) {
-            unsigned char* sws = nullptr;
-            u32 parity = 0, tag = 0;
-            if ((rc = slot.spec(hi - lo, nseg, &sws, &parity, &tag))) return rc;
-            ++ws_stat_spec_calls;
-            rc = ws_launch_piece_spec(L, lo, hi, sws, parity, tag, (u32)hint, adv_d);
-            if (rc) slot.spec_failed();
-            return rc;
-        }
+        // captured calls have no advice word: their K1 starts with no stride guess
+        if (!capturing(stream) && (rc = slot.advice(&adv_h, &adv_d))) return rc;
         if (need && (rc = slot.workspace(need, 16, &ws))) return rc;
     }
-    ++ws_stat_classic_calls;
     const u32 gen = ws_next_gen();
     const u32* disorder = nullptr;
     bool fallback = false;

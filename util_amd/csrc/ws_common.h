@@ -107,8 +107,8 @@ __device__ __forceinline__ void ws_hdr_from32(const u32x4 x0, const u32x4 x1, u3
 }
 
 // The wire length of the batch's first frame (of the first segment with >= 2 bytes among the
-// first 8), 0 unless it is a plain complete frame: the speculative piece path's frame-length
-// hint for the next call on the stream (ws_spec.hip). One thread.
+// first 8), 0 unless it is a plain complete frame: K1's first-step stride guess for the next
+// call on the stream (ws_piece.hip; a wrong guess costs loads only). One thread.
 __device__ __forceinline__ u32 ws_first_frame_len(const unsigned char* buf, const u64* seg_off, const u64* seg_len,
                                                   u32 nseg) {
     for (u32 s = 0; s < nseg && s < 8; ++s) {
@@ -389,13 +389,6 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
                          bool count_nonuniform = false, u32 g0 = 0);
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr);
 int ws_piece_dyn_lds(const WsLaunch& L);
-// the speculative piece path (ws_spec.hip): no K1; sws = the slot's spec workspace
-size_t ws_spec_workspace_bytes(u64 span, u32 nseg);
-size_t ws_spec_zero_bytes(u32 nseg);
-bool ws_spec_fits(u64 span, u32 nseg);
-size_t ws_spec_flags_off();
-int ws_launch_piece_spec(const WsLaunch& L, u64 lo, u64 hi, unsigned char* sws, u32 parity, u32 tag, u32 g,
-                         int* advice_dev);
 u32 ws_next_gen();
 int ws_device_info(int* cus, int* lds_per_cu);
 // auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are zero at allocation +
@@ -421,9 +414,7 @@ struct WsSlot {
     int workspace(size_t bytes, size_t zero_bytes, void** out);   // decode / reassembly / stream
     int encode_workspace(size_t bytes, void** out);
     int aux(size_t dbytes, size_t hbytes, WsAux* out);
-    int advice(int** host, int** dev);                             // the path advice word (eager)
-    int spec(u64 span, u32 nseg, unsigned char** sws, u32* parity, u32* tag);
-    void spec_failed();
+    int advice(int** host, int** dev);                             // the stride hint words (eager)
 };
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,

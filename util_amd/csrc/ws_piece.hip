@@ -16,7 +16,8 @@
 //   it. A segment that starts before the previous one ends (or lies outside [lo, hi))
 //   marks the batch unordered. It also counts the segments whose frames are not all of
 //   the first frame's length (or that stop on an error): K2 turns that count into the
-//   host's advice to take the speculative path (ws_spec.hip, no K1) on the next call.
+//   host's hint for the next call's first step (g0 below: the first frame's length, used
+//   only while nearly every segment is uniform).
 // K2 ws_piece_unmask_kernel — one 256-thread block per piece, 4 chunks per lane:
 //   payload loads first, then (while they are in flight) the piece pointer and the
 //   items it leads to (16, then 64 per load, hopping to the next segment when the piece
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         for (u32 s2 = blockIdx.x * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
             walk_segment<4, NT>(buf, s2, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
     }
-    // the host's next path choice (ws_api.hip): speculative while at most 1/32 of the
+    // the host's stride hint for the next call (ws_api.hip): valid while at most 1/32 of the
     // segments had frames of more than one length (K1 has finished: its count is final)
     if (advice && bx == 0 && tid == 0) {
         const u32 n = *gptr<u32>(nonuni);
@@ -389,7 +390,7 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     return 0;
 }
 
-// "piece_lds": bytes of unused dynamic LDS per K2 (and speculative S1) block, which caps its
+// "piece_lds": bytes of unused dynamic LDS per K2 block, which caps its
 // blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 6 — K2 needs only 60 VGPRs
 // (8 waves/SIMD would fit) but streams best at 6 blocks per CU in round 3 (cfg2 K1 + K2
 // 1.355 ms at 6 against 1.375-1.378 at 4 and 5, 1.374 at 7, 1.40 at 8, interleaved in one
@@ -407,7 +408,7 @@ int ws_piece_dyn_lds(const WsLaunch& L) {
 }
 
 // "k2_timing" (measurement only, bench.py): a pair of HIP events is recorded around every
-// K2 (or S1) launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
+// K2 launch on its stream; websocketframeGpuGetStat("k2_ns") waits for and sums the
 // recorded durations, "k2_calls" counts them; setting the option clears the record.
 WsOpt ws_k2_timing{0};
 static std::vector<hipEvent_t> g_k2ev;    // start, end, start, end, ...
@@ -449,7 +450,7 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
 }
 
 // K2 over the pieces of a scanned batch; advice (device view of pinned host memory, may be
-// null): K2 turns K1's non-uniform count into the host's next path choice
+// null): K2 turns K1's non-uniform count into the host's stride hint for the next call
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice) {
     if (!P.npieces) return 0;
     size_t tslot = 0;
