@@ -37,65 +37,113 @@
 static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's chunks");
 #define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
 
+// ---- hand-off helpers of the fused form (ws_piece_fused_kernel below). Walker waves publish with
+// write-through (sc1) stores, wait for them (vmcnt(0)), then store a generation-tagged word; the
+// unmask waves poll tagged words with scalar loads that bypass the scalar cache (glc) and read the
+// published items with sc1 vector loads (L1 bypass): MI355X_MICROARCH.md, "Workgroup dispatch, XCD
+// placement & inter-workgroup visibility", hand-off form of row 1 (hipMalloc memory).
+__device__ __forceinline__ void st16_sc1(gu32x4* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 ld16_sc1(const gu32x4* p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u32x4 sld16_glc(const void* p) {
+    u32x4 v;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u64 sld8_glc(const void* p) {
+    u64 v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // item: w0 = P0 | rkey[15:0] << 48, w1 = P1 | rkey[31:16] << 48 (origin-relative bytes < 2^48)
+template <bool FUSED>
 __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
     const u64 w0 = p0 | ((u64)(rk & 0xFFFFu) << 48), w1 = p1 | ((u64)(rk >> 16) << 48);
     u32x4 q;
     q.x = (u32)w0; q.y = (u32)(w0 >> 32); q.z = (u32)w1; q.w = (u32)(w1 >> 32);
-    *it = q;
+    if (FUSED) st16_sc1(it, q);
+    else *it = q;
 }
 
-// pieces whose first byte is in [lo, hi) (origin-relative) get `val`; only pieces of the
-// batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the
-// batch unordered, and its pointers are clipped here)
-__device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u64 val) {
+// pieces whose first byte is in [lo, hi) (origin-relative) get segment s, item k; only pieces
+// of the batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the
+// batch unordered, and its pointers are clipped here). Classic table: one u64 s << 32 | k per
+// piece. Fused table: 16 B {s, tag, k, tag} per piece, stored write-through (each 8-B half
+// carries the call's tag, so a half read before the store lands is never taken as current).
+template <bool FUSED>
+__device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u32 tag) {
     u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
-    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi && p < pend; ++p) *gptr<u64>(ptr + (p - pbase)) = val;
+    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi && p < pend; ++p) {
+        if (FUSED) {
+            u32x4 q;
+            q.x = s; q.y = tag; q.z = k; q.w = tag;
+            st16_sc1(gptr<u32x4>(reinterpret_cast<u32x4*>(ptr) + (p - pbase)), q);
+        } else {
+            *gptr<u64>(reinterpret_cast<u64*>(ptr) + (p - pbase)) = ((u64)s << 32) | k;
+        }
+    }
 }
 
-// K1: G = 16 lanes per segment, header walk by STRIDE SPECULATION: lane k of the group
-// parses the header at off + k*g (g = the last frame's length); the chain is right up
-// to the first lane whose frame length differs (ballot), so a run of up to G equal frames
-// is walked in one round trip and its items, descriptors and piece pointers are written
-// by the lanes in parallel. 16 keeps four segments in flight per wave (the walk is
-// latency-bound; 8, 32, 64 lanes and one lane per segment measured slower in round 1).
-#define PSCAN_T 256
-template <int G>
-__global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned char* __restrict__ buf,
-                                                                const u64* __restrict__ seg_off,
-                                                                const u64* __restrict__ seg_len, u32 nseg,
-                                                                u32 max_frames, const u64* __restrict__ desc_base,
-                                                                WebsocketFrameDesc_t* __restrict__ desc,
-                                                                WebsocketSegResult_t* __restrict__ res,
-                                                                u32x4* __restrict__ items, u32* __restrict__ nwork,
-                                                                u64* __restrict__ ptr, u32* __restrict__ disorder,
-                                                                u32 gen, u64 pbase, u64 lo, u64 hi, u32* nonuni,
-                                                                u32 g0, WsSegRec* __restrict__ segr) {
-    static_assert(G == 16, "group size");
-    const u32 lane = threadIdx.x & 63;
+// What one segment walk needs (K1, and the walker blocks of the fused kernel).
+struct WalkArgs {
+    const unsigned char* buf;
+    const u64* seg_off;
+    const u64* seg_len;
+    u32 nseg, max_frames;
+    const u64* desc_base;
+    WebsocketFrameDesc_t* desc;
+    WebsocketSegResult_t* res;
+    u32x4* items;
+    void* ptr;            // classic u64 table or fused 16-B table
+    u32* nwork;           // classic only
+    WsSegRec* segr;       // classic only
+    u32* disorder;        // classic only (the fused kernel checks the order in a phase of its own)
+    u32 gen;
+    u64 pbase, lo, hi;
+    u32 g0;
+};
+
+// G = 16 lanes per segment, header walk by STRIDE SPECULATION: lane k of the group parses the
+// header at off + k*g (g = the last frame's length); the chain is right up to the first lane
+// whose frame length differs (ballot), so a run of up to G equal frames is walked in one round
+// trip and its items, descriptors and piece pointers are written by the lanes in parallel. 16
+// keeps four segments in flight per wave (the walk is latency-bound; 8, 32, 64 lanes and one
+// lane per segment measured slower in round 1). The group's segment is s (active groups); on
+// return lane gl == 0 of the group holds its item count and whether its frames were not all of
+// one length (or it stopped on an error).
+#define WALK_G 16
+template <bool FUSED>
+__device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active, u32 lane, u32& cnt_out,
+                                           bool& nonu_out) {
+    constexpr u32 G = WALK_G;
     const u32 gl = lane % G, gb = lane - gl;                                 // lane in group, group's first lane
-    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / G;
-    bool active = s < nseg;
-    const u32 sc = active ? s : nseg - 1;                                    // inactive groups: harmless loads
-    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
-    const u64 pend = hi + lead0 ? ((hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
-    const u64 so = seg_off[sc], sl = seg_len[sc];
-    const u64 prev_end = sc ? seg_off[sc - 1] + seg_len[sc - 1] : 0;
-    if (active && gl == 0 && (prev_end > so || so < lo || so > hi || sl > hi - so)) *gptr<u32>(disorder) = gen;
-    const u64 dbase = desc_base ? desc_base[sc] : (u64)sc * max_frames;
-    const u64 ibase = (u64)sc * max_frames;
+    const u32 sc = active ? s : A.nseg - 1;                                  // inactive groups: harmless loads
+    const u64 lead0 = reinterpret_cast<uintptr_t>(A.buf) & 15;
+    const u64 pend = A.hi + lead0 ? ((A.hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
+    const u64 so = A.seg_off[sc], sl = A.seg_len[sc];
+    const u64 prev_end = sc ? A.seg_off[sc - 1] + A.seg_len[sc - 1] : 0;
+    if (!FUSED && active && gl == 0 && (prev_end > so || so < A.lo || so > A.hi || sl > A.hi - so))
+        *gptr<u32>(A.disorder) = A.gen;
+    const u64 dbase = A.desc_base ? A.desc_base[sc] : (u64)sc * A.max_frames;
+    const u64 ibase = (u64)sc * A.max_frames;
     const u64 sorg = so + lead0;
-    const u64 tag = (u64)sc << 32;
-    const uintptr_t seg = reinterpret_cast<uintptr_t>(buf + so);
-    if (active && gl == 0) put_ptrs(ptr, pbase, pend, s ? prev_end + lead0 : 0, sorg, tag);
+    const uintptr_t seg = reinterpret_cast<uintptr_t>(A.buf + so);
+    if (active && gl == 0) put_ptrs<FUSED>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, A.gen);
     // g0: the stride guess of the first step (the host's hint, 0 = none): lane k parses off + k*g0
     // at once; lane 0's frame is always the true first one, so a wrong guess costs nothing but
     // its loads (code 1 at lane 0 takes the true length)
-    u64 off = 0, g = g0, walked_end = sorg;
+    u64 off = 0, g = A.g0, walked_end = sorg;
     u32 nf = 0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
     bool nonu = false;                       // frames of another length than the first, or an error stop
-    const u64 gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+    const u64 gmask = (1ull << G) - 1;
     while (__ballot(active)) {
         const u64 pos = off + (u64)gl * g;                                  // candidate frame offset
         const bool cand = active && (gl == 0 || g > 0);
@@ -113,7 +161,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         int st = WEBSOCKET_SEG_OK;
         if (cand) {
             if (pos >= sl) code = 3;
-            else if (nf + gl >= max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
+            else if (nf + gl >= A.max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
             else if (sl - pos < 2) code = 3;                                 // websocketframe.c:121
             else if (h.kind == WS_PARSE_INCOMPLETE) code = 3;
             else if (h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
@@ -121,7 +169,7 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
             else code = (u64)(u32)h.ret == g ? 0u : 1u;
         }
         const u64 stop = (__ballot(code != 0) >> gb) & gmask;
-        const u32 mm = stop ? (u32)__builtin_ctzll(stop) : (u32)G;         // first non-continuing lane
+        const u32 mm = stop ? (u32)__builtin_ctzll(stop) : G;              // first non-continuing lane
         const u32 src = gb + (mm < G ? mm : G - 1);
         const u32 code_m = mm < G ? (u32)__shfl((int)code, (int)src) : 0u;
         const int ret_m = __shfl(h.ret, (int)src);
@@ -130,9 +178,10 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
         if (gl < ntake) {                                                   // consumed frames, in parallel
-            put_item(gptr<u32x4>(items + ibase + nf + gl), p0, h.masked ? fe : p0, rotl32(h.key, 8u * (u32)(p0 & 3)));
-            put_ptrs(ptr, pbase, pend, fo, fe, tag | (nf + gl));
-            if (h.ret != 0) ws_store_desc(desc + dbase + nf + gl, so + pos, h);
+            put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + gl), p0, h.masked ? fe : p0,
+                            rotl32(h.key, 8u * (u32)(p0 & 3)));
+            put_ptrs<FUSED>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, A.gen);
+            if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + gl, so + pos, h);
         }
         const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
         if (ntake) walked_end = fe_last;
@@ -162,48 +211,109 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(const unsigned c
         active = false;
         if (gl == 0) {
             const u32 cnt = nf + extra;
-            put_ptrs(ptr, pbase, pend, walked_end, sorg + sl, tag | cnt);         // pieces starting in the tail
-            if (s == nseg - 1) put_ptrs(ptr, pbase, pend, sorg + sl, hi + lead0, PIECE_NONE);
-            ws_store_res(res + s, off, nf, status);
-            *gptr<u32>(nwork + s) = cnt;
-            put_item(gptr<u32x4>(reinterpret_cast<u32x4*>(segr + s)), sorg, sorg + sl, cnt);   // WsSegRec
+            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt, A.gen);   // pieces starting in the tail
+            if (sc == A.nseg - 1)
+                put_ptrs<FUSED>(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, A.gen);
+            ws_store_res(A.res + sc, off, nf, status);
+            if (!FUSED) {
+                *gptr<u32>(A.nwork + sc) = cnt;
+                put_item<false>(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)), sorg, sorg + sl, cnt);   // WsSegRec
+            }
+            cnt_out = cnt;
+            nonu_out = nonu;
         }
     }
+}
+
+// K1: one walk per segment (16 lanes each); counts the segments whose frames are not all of one
+// length for the K2 that follows (nonuni, may be null)
+#define PSCAN_T 256
+__global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(WalkArgs A, u32* nonuni) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / WALK_G;
+    u32 cnt = 0;
+    bool nonu = false;
+    walk_group<false>(A, s, s < A.nseg, lane, cnt, nonu);
     if (nonuni) {                                                           // one atomic per wave, if any
-        const u64 b = __ballot(gl == 0 && s < nseg && nonu);
+        const u64 b = __ballot(lane % WALK_G == 0 && s < A.nseg && nonu);
         if (lane == 0 && b) atomicAdd(nonuni, (u32)__popcll(b));
     }
 }
 
-// K2. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
+// K2's inputs (the classic kernel and the unmask blocks of the fused one)
+struct UnmaskArgs {
+    unsigned char* buf;
+    const u64* seg_off;
+    const u64* seg_len;
+    u32 nseg, max_frames;
+    const u32x4* items;
+    const u32* nwork;
+    const void* ptr;              // classic u64 table or fused 16-B table
+    const u32* disorder;
+    u32 gen;
+    u64 pbase, c_lo, c_hi;
+    const u64* desc_base;
+    WebsocketFrameDesc_t* desc;
+    WebsocketSegResult_t* res;
+    u32 wshift;
+    u64 ppw, npieces;
+    u32* nonuni;
+    int* advice;
+    const WsSegRec* segr;
+    // fused kernel only
+    const u64* done;              // per segment: cnt | tag << 32, stored once the segment's items are out
+    struct FusedHead* head;
+    u32 nwb;                      // walker blocks in front of the unmask blocks
+};
+
+// The fused kernel's head (its buffer's first 64 B, zeroed at allocation): the counters rest at
+// zero between calls (the last arriver resets them); the words are generation-tagged.
+struct FusedHead {
+    u64 verdict;                  // gen << 1 | unordered: the order check's outcome
+    u32 cnt_check;                // walker blocks done with the order check
+    u32 cnt_done;                 // walker blocks done walking
+    u32 disw;                     // = gen: some walker block found the segments unordered
+    u32 nonuni;                   // segments whose frames are not all of one length
+    u32 donew;                    // = gen: every walker block is done
+    u32 fails;                    // unmask waves that gave up waiting (never expected)
+    u32 pad[8];
+};
+static_assert(sizeof(FusedHead) == 64, "fused head");
+#define FUSED_SPINS (1u << 16)    // polls (s_sleep 2 each) before a wave gives up waiting (tens of ms)
+
+// poll a tagged word (scalar, wave-uniform): true when current, false when the wait gave up
+__device__ __forceinline__ bool poll_done(const u64* done, u32 s, u32 gen, u32& cnt) {
+    for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
+        const u64 d = sld8_glc(done + s);
+        if ((u32)(d >> 32) == gen) {
+            cnt = (u32)d;
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+// K2 body. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
 // exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
 // all measured slower): nontemporal loads and stores, chunks wholly inside
 // segments stored whole (byte coverage by the visited segments), 2^wshift windows.
-template <int NT, int SR>
-__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
-                                                                  const u64* __restrict__ seg_off,
-                                                                  const u64* __restrict__ seg_len, u32 nseg,
-                                                                  u32 max_frames, const u32x4* __restrict__ items,
-                                                                  const u32* __restrict__ nwork,
-                                                                  const u64* __restrict__ ptr,
-                                                                  const u32* __restrict__ disorder, u32 gen, u64 pbase,
-                                                                  u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
-                                                                  WebsocketFrameDesc_t* __restrict__ desc,
-                                                                  WebsocketSegResult_t* __restrict__ res,
-                                                                  u32 wshift, u64 ppw, u64 npieces, u32* nonuni,
-                                                                  int* advice, const WsSegRec* __restrict__ segr) {
+// FUSED: the piece pointer, the order verdict and each segment's item count come from walker
+// blocks of the same launch (tagged words, polled); the items are read write-through.
+template <int NT, int SR, bool FUSED>
+__device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
-    const u32 bx = blockIdx.x;
-    const u64 pw = (u64)(bx & ((1u << wshift) - 1u)) * ppw + (bx >> wshift);
-    const bool pvalid = pw < npieces;
-    const u64 pidx = pvalid ? pw : npieces - 1;
-    const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
+    const u64 pw = (u64)(bx & ((1u << A.wshift) - 1u)) * A.ppw + (bx >> A.wshift);
+    const bool pvalid = pw < A.npieces;
+    const u64 pidx = pvalid ? pw : A.npieces - 1;
+    const u64 pc0 = (A.pbase + pidx) << (PIECE_SHIFT - 4);                   // first chunk of the piece
     const u64 wc0 = pc0 + (u64)wv * (64 * PIECE_U);                          // this wave's 4 KiB: 256 chunks
-    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(A.buf) & ~(uintptr_t)15);
+    const u64 c_lo = A.c_lo, c_hi = A.c_hi;
     // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
     u32x4 v[PIECE_U];
 #pragma unroll
@@ -214,26 +324,62 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     // ---- 2. items that touch this wave's range [r0, r1) (origin-relative bytes)
     constexpr long long RW = 64 * PIECE_U * 16;                             // this wave's bytes
     const u64 r0 = wc0 << 4, r1 = r0 + RW;
-    const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-        reinterpret_cast<uintptr_t>(ptr + pidx));
-    // the next piece's first item: when it is in the same segment, the items that touch this
-    // piece are exactly [k, k_next], so the first load takes only those (long segments would
-    // otherwise load 16 per wave however few they need)
-    const u64 pn = pidx + 1 < npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-                                            reinterpret_cast<uintptr_t>(ptr + pidx + 1))
-                                      : PIECE_NONE;
-    const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
+    const u32 nseg = A.nseg;
+    u32 s = nseg, k = 0, step = 16;
+    bool exact = false;                                                     // the first load holds them all
+    bool ok = false, failed = false;
+    if (FUSED) {
+        // the order verdict and this piece's pointer (the next piece's too, if already current:
+        // it bounds the first item load, as below)
+        const u32 gen = A.gen;
+        const u32x4* pt = reinterpret_cast<const u32x4*>(A.ptr);
+        u32x4 pv = {0, 0, 0, 0};
+        failed = true;
+        for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
+            const u64 vd = sld8_glc(&A.head->verdict);
+            pv = sld16_glc(pt + pidx);
+            if ((u32)(vd >> 1) == gen && ((vd & 1) || (pv.y == gen && pv.w == gen))) {
+                failed = false;
+                ok = !(vd & 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (ok && pvalid && pv.x != 0xFFFFFFFFu) {
+            s = pv.x;
+            k = pv.z;
+            if (pidx + 1 < A.npieces) {
+                const u32x4 pn = sld16_glc(pt + pidx + 1);
+                if (pn.y == gen && pn.w == gen && pn.x == s && pn.z >= k && pn.z - k < 16u) {
+                    step = pn.z - k + 1;
+                    exact = true;
+                }
+            }
+        }
+    } else {
+        const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+            reinterpret_cast<uintptr_t>(reinterpret_cast<const u64*>(A.ptr) + pidx));
+        // the next piece's first item: when it is in the same segment, the items that touch this
+        // piece are exactly [k, k_next], so the first load takes only those (long segments would
+        // otherwise load 16 per wave however few they need)
+        const u64 pn = pidx + 1 < A.npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+                                                  reinterpret_cast<uintptr_t>(reinterpret_cast<const u64*>(A.ptr) + pidx + 1))
+                                            : PIECE_NONE;
+        ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(A.disorder)) != A.gen;
+        // no early return: an exit branch here would be hoisted above the payload loads
+        if (ok && pvalid && pv != PIECE_NONE) {
+            s = (u32)(pv >> 32);
+            k = (u32)pv;
+        }
+        if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
+            step = (u32)pn - k + 1;
+            exact = true;
+        }
+    }
     u32 cov[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) cov[u] = 0;
-    // no early return: an exit branch here would be hoisted above the payload loads
-    u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv, step = 16;
-    bool exact = false;                                                     // the first load holds them all
-    if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
-        step = (u32)pn - k + 1;
-        exact = true;
-    }
-    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(A.buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
     // (bytes the decode does not change are written back unchanged: one 16-B store
@@ -249,15 +395,20 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
         u32 cnt;
         if (SR) {
             const u32x4 R = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(
-                reinterpret_cast<uintptr_t>(segr + s));
+                reinterpret_cast<uintptr_t>(A.segr + s));
             const u64 w0 = (u64)R.x | ((u64)R.y << 32), w1 = (u64)R.z | ((u64)R.w << 32);
             slo = w0 & 0xFFFFFFFFFFFFull; shi = w1 & 0xFFFFFFFFFFFFull;
             cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
         } else {
-            slo = seg_off[s] + lead0; shi = slo + seg_len[s]; cnt = nwork[s];
+            slo = A.seg_off[s] + lead0; shi = slo + A.seg_len[s];
+            if (!FUSED) cnt = A.nwork[s];
         }
         if (!first && slo >= r1) break;                                     // the next segment starts past us
         first = false;
+        if (FUSED && !poll_done(A.done, s, A.gen, cnt)) {
+            failed = true;
+            break;
+        }
         {
             // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
             const long long sa = (long long)(slo - r0), sb = (long long)(shi - r0);
@@ -277,7 +428,10 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             const u32 j = k + lane;
             const bool valid = j < cnt && lane < step;
             u32x4 q = {0, 0, 0, 0};
-            if (valid) q = items[(u64)s * max_frames + j];
+            if (valid) {
+                if (FUSED) q = ld16_sc1(gptr<u32x4>(A.items + (u64)s * A.max_frames + j));
+                else q = A.items[(u64)s * A.max_frames + j];
+            }
             const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
             const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
             const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
@@ -286,13 +440,13 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
             // wave-relative item range, clamped to [-16, RW + 16] (32-bit from here on)
             const long long ra = (long long)(P0 - r0), rb = (long long)(P1 - r0);
-            const int A = (int)(ra < -16 ? -16 : (ra > RW + 16 ? RW + 16 : ra));
-            const int B = (int)(rb < -16 ? -16 : (rb > RW + 16 ? RW + 16 : rb));
+            const int Ai = (int)(ra < -16 ? -16 : (ra > RW + 16 ? RW + 16 : ra));
+            const int Bi = (int)(rb < -16 ? -16 : (rb > RW + 16 ? RW + 16 : rb));
             u64 hm = __ballot(valid && lane < nlim && P1 > r0 && P0 < P1);
             while (hm) {
                 const int i = __builtin_ctzll(hm);
                 hm &= hm - 1;
-                const int a = __builtin_amdgcn_readlane(A, i), b = __builtin_amdgcn_readlane(B, i);
+                const int a = __builtin_amdgcn_readlane(Ai, i), b = __builtin_amdgcn_readlane(Bi, i);
                 const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
 #pragma unroll
                 for (int u = 0; u < PIECE_U; ++u) {
@@ -313,31 +467,147 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     }
     // ---- 3. store (v[] holds the unmasked bytes): full chunks one 16-B store, edge chunks
     //         exactly the covered bytes
+    if (!failed) {
 #pragma unroll
-    for (int u = 0; u < PIECE_U; ++u) {
-        const u64 c = wc0 + (u64)(u * 64 + lane);
-        if (!cov[u] || c < c_lo || c >= c_hi) continue;
-        const u32x4 w = v[u];
-        if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
-            st16<NT>(w, base + c);
-        } else {
-            ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
+        for (int u = 0; u < PIECE_U; ++u) {
+            const u64 c = wc0 + (u64)(u * 64 + lane);
+            if (!cov[u] || c < c_lo || c >= c_hi) continue;
+            const u32x4 w = v[u];
+            if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
+                st16<NT>(w, base + c);
+            } else {
+                ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
+            }
         }
+    } else if (lane == 0) {
+        atomicAdd(&A.head->fails, 1u);                                      // nothing stored: the stat shows it
     }
-    // K1 found the segments out of buffer order (or outside [lo, hi)): nothing was stored
-    // above; the batch is decoded here instead, one wavefront per segment (ws_walk.h)
-    if (!ok) {
-        for (u32 s2 = blockIdx.x * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
-            walk_segment<4, NT>(buf, s2, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
+    // the segments are out of buffer order (or outside [lo, hi)): nothing was stored above; the
+    // batch is decoded here instead, one wavefront per segment (ws_walk.h). Fused: once every
+    // walker block is done (their descriptors are then final, and these walks rewrite them).
+    if (!ok && !failed) {
+        const u32 nblk = gridDim.x - (FUSED ? A.nwb : 0u);
+        bool go = true;
+        if (FUSED) {
+            go = false;
+            for (u32 spins = 0; spins < FUSED_SPINS && !go; ++spins) {
+                go = (u32)sld8_glc(&A.head->donew) == A.gen;
+                if (!go) __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (go)
+            for (u32 s2 = bx * (PIECE_T / 64) + wv; s2 < nseg; s2 += nblk * (PIECE_T / 64))
+                walk_segment<4, NT>(A.buf, s2, A.seg_off, A.seg_len, A.max_frames, A.desc_base, A.desc, A.res, lane);
     }
     // the host's stride hint for the next call (ws_api.hip): valid while at most 1/32 of the
     // segments had frames of more than one length (K1 has finished: its count is final)
-    if (advice && bx == 0 && tid == 0) {
-        const u32 n = *gptr<u32>(nonuni);
-        *gptr<u32>(nonuni) = 0;
-        __hip_atomic_store(advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(advice + 1, (int)ws_first_frame_len(buf, seg_off, seg_len, nseg), __ATOMIC_RELAXED,
+    if (!FUSED && A.advice && bx == 0 && tid == 0) {
+        const u32 n = *gptr<u32>(A.nonuni);
+        *gptr<u32>(A.nonuni) = 0;
+        __hip_atomic_store(A.advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(A.advice + 1, (int)ws_first_frame_len(A.buf, A.seg_off, A.seg_len, nseg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <int NT, int SR>
+__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(UnmaskArgs A) {
+    unmask_piece<NT, SR, false>(A, blockIdx.x);
+}
+
+// Segment index of walker task t: the tasks alternate between the segments from the start of the
+// batch (A = [0, s1)) and those from the middle (B = [s1, nseg), s1 ~ where K2's second window
+// starts), the order in which the unmask blocks' two windows reach them; the rest in order.
+__device__ __forceinline__ u32 task_seg(u64 t, u32 s1, u32 nseg) {
+    const u32 na = s1, nb = nseg - s1, m = na < nb ? na : nb;
+    if (t < 2ull * m) return (t & 1) ? s1 + (u32)(t >> 1) : (u32)(t >> 1);
+    const u32 r = (u32)(t - 2ull * m);
+    return na > nb ? m + r : s1 + m + r;
+}
+
+// The fused decode: K1's walks and K2's unmask in ONE launch. Blocks [0, nwb) are walker blocks:
+// (1) each checks the order of its share of the segment table, the last one to finish publishes
+// the verdict; (2) 16-lane groups walk the segments (walk_group, write-through items and tagged
+// piece pointers, then per segment a tagged item count) in the order the unmask blocks reach
+// them; (3) the last walker block to finish writes the host's stride hint. Blocks [nwb, grid) are
+// K2's unmask blocks: each issues its payload loads first, then polls its piece's pointer and
+// segment counts (walkers run ahead: dispatched first, they never wait on anything).
+__global__ __launch_bounds__(PIECE_T) void ws_piece_fused_kernel(WalkArgs W, UnmaskArgs A) {
+    if (blockIdx.x >= A.nwb) {
+        unmask_piece<1, 0, true>(A, blockIdx.x - A.nwb);
+        return;
+    }
+    const u32 tid = threadIdx.x, lane = tid & 63, b = blockIdx.x, nwb = A.nwb, nseg = A.nseg;
+    FusedHead* const H = A.head;
+    // (1) order check of segments [b * chunk, (b + 1) * chunk)
+    const u32 chunk = (nseg + nwb - 1) / nwb;
+    const u64 sb = (u64)b * chunk, se0 = sb + chunk, se = se0 < nseg ? se0 : nseg;
+    bool bad = false;
+    for (u64 s = sb + tid; s < se; s += PIECE_T) {
+        const u64 so = W.seg_off[s], sl = W.seg_len[s];
+        const u64 prev_end = s ? W.seg_off[s - 1] + W.seg_len[s - 1] : 0;
+        bad |= prev_end > so || so < W.lo || so > W.hi || sl > W.hi - so;
+    }
+    if (__ballot(bad) && lane == 0) __hip_atomic_store(&H->disw, A.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wait_stores();
+    __syncthreads();
+    if (tid == 0) {
+        const u32 old = __hip_atomic_fetch_add(&H->cnt_check, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nwb - 1) {
+            __hip_atomic_store(&H->cnt_check, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32 d = __hip_atomic_load(&H->disw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&H->verdict, ((u64)A.gen << 1) | (d == A.gen ? 1ull : 0ull), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // (2) segment walks, 16 lanes each; a wave publishes its four segments' counts once its own
+    // stores have landed
+    // s1 ~ the first segment of the unmask blocks' second window: one interpolation step from the
+    // middle of the table (it orders the walks only; any value gives the same result)
+    u32 s1 = nseg;
+    if (A.wshift == 1) {
+        const u64 lead0 = reinterpret_cast<uintptr_t>(W.buf) & 15;
+        const u64 x1 = ((A.pbase + A.ppw) << PIECE_SHIFT) - lead0;
+        const u32 sg = nseg / 2;
+        const u64 first = W.seg_off[0], last = W.seg_off[nseg - 1] + W.seg_len[nseg - 1];
+        const long long avg = last > first && (last - first) / nseg > 0 ? (long long)((last - first) / nseg) : 1;
+        long long g = (long long)sg + ((long long)x1 - (long long)W.seg_off[sg]) / avg;
+        s1 = (u32)(g < 0 ? 0 : (g > (long long)nseg ? (long long)nseg : g));
+    }
+    const u64 NG = (u64)nwb * (PIECE_T / WALK_G);
+    const u64 gg = (u64)b * (PIECE_T / WALK_G) + tid / WALK_G;
+    u32 nonu_n = 0;
+    for (u64 t = gg;; t += NG) {
+        const bool act = t < nseg;
+        if (!__ballot(act)) break;
+        const u32 s = act ? task_seg(t, s1, nseg) : nseg - 1;
+        u32 cnt = 0;
+        bool nonu = false;
+        walk_group<true>(W, s, act, lane, cnt, nonu);
+        wait_stores();
+        if (act && lane % WALK_G == 0)
+            __hip_atomic_store(const_cast<u64*>(A.done) + s, ((u64)A.gen << 32) | cnt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        nonu_n += (u32)__popcll(__ballot(act && lane % WALK_G == 0 && nonu));
+    }
+    // (3) the last walker block: stride hint, and the word the unordered fallback waits for
+    if (lane == 0 && nonu_n) __hip_atomic_fetch_add(&H->nonuni, nonu_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wait_stores();
+    __syncthreads();
+    if (tid == 0) {
+        const u32 old = __hip_atomic_fetch_add(&H->cnt_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nwb - 1) {
+            __hip_atomic_store(&H->cnt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32 n = __hip_atomic_exchange(&H->nonuni, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64 vd = __hip_atomic_load(&H->verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (A.advice) {
+                __hip_atomic_store(A.advice, !(vd & 1) && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(A.advice + 1, (int)ws_first_frame_len(W.buf, W.seg_off, W.seg_len, nseg),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __hip_atomic_store(&H->donew, A.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -379,11 +649,14 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     P.segr = reinterpret_cast<WsSegRec*>(ws + b);
     b += (size_t)L.nseg * sizeof(WsSegRec);
     P.items = reinterpret_cast<u32x4*>(ws + b);
-    const u32 blocks = (u32)(((u64)L.nseg * 16 + PSCAN_T - 1) / PSCAN_T);
-    hipLaunchKernelGGL(ws_piece_scan_kernel<16>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, L.buf, L.seg_off,
-                       L.seg_len, L.nseg, L.max_frames, L.desc_base, L.desc, L.res, P.items, P.nwork, P.ptr,
-                       P.disorder, gen, P.pbase, lo, hi, count_nonuniform ? P.nonuni : nullptr,
-                       g0 < (1u << 31) ? g0 : 0u, P.segr);
+    const u32 blocks = (u32)(((u64)L.nseg * WALK_G + PSCAN_T - 1) / PSCAN_T);
+    WalkArgs W;
+    W.buf = L.buf; W.seg_off = L.seg_off; W.seg_len = L.seg_len; W.nseg = L.nseg; W.max_frames = L.max_frames;
+    W.desc_base = L.desc_base; W.desc = L.desc; W.res = L.res; W.items = P.items; W.ptr = P.ptr; W.nwork = P.nwork;
+    W.segr = P.segr; W.disorder = P.disorder; W.gen = gen; W.pbase = P.pbase; W.lo = lo; W.hi = hi;
+    W.g0 = g0 < (1u << 31) ? g0 : 0u;
+    hipLaunchKernelGGL(ws_piece_scan_kernel, dim3(blocks), dim3(PSCAN_T), 0, L.stream, W,
+                       count_nonuniform ? P.nonuni : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
     *out = P;
@@ -449,28 +722,39 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
     return 0;
 }
 
+static UnmaskArgs unmask_args(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice, u32 wshift, u64 ppw) {
+    UnmaskArgs A;
+    A.buf = L.buf; A.seg_off = L.seg_off; A.seg_len = L.seg_len; A.nseg = L.nseg; A.max_frames = L.max_frames;
+    A.items = P.items; A.nwork = P.nwork; A.ptr = P.ptr; A.disorder = P.disorder; A.gen = gen; A.pbase = P.pbase;
+    A.c_lo = P.c_lo; A.c_hi = P.c_hi; A.desc_base = L.desc_base; A.desc = L.desc; A.res = L.res; A.wshift = wshift;
+    A.ppw = ppw; A.npieces = P.npieces; A.nonuni = P.nonuni; A.advice = advice; A.segr = P.segr;
+    A.done = nullptr; A.head = nullptr; A.nwb = 0;
+    return A;
+}
+
+static u32 piece_wshift(u64 npieces) {
+    const int pwin = ws_piece_win;
+    u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
+    while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
+    return wshift;
+}
+
 // K2 over the pieces of a scanned batch; advice (device view of pinned host memory, may be
 // null): K2 turns K1's non-uniform count into the host's stride hint for the next call
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice) {
     if (!P.npieces) return 0;
     size_t tslot = 0;
     int rc;
-    const int timing = ws_k2_timing, pwin = ws_piece_win;
+    const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
-    while (wshift && (P.npieces >> wshift) < 256) --wshift;              // small batches: one window
+    const u32 wshift = piece_wshift(P.npieces);
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
+    UnmaskArgs A = unmask_args(L, P, gen, advice, wshift, ppw);
     if (P.segr)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
-                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
-                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
-                           advice, (const WsSegRec*)P.segr);
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, A);
     else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
-                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
-                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
-                           advice, (const WsSegRec*)nullptr);
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, A);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
     return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
@@ -487,4 +771,65 @@ int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 ge
     *disorder_out = P.disorder;
     *fallback_needed = P.npieces == 0;
     return 0;
+}
+
+// ---- the fused form (one launch: walker blocks + unmask blocks, ws_piece_fused_kernel)
+// buffer: [FusedHead 64 B][ptr: npieces x 16 B][done: nseg x 8 B, 16-B aligned][items: nseg*max_frames x 16 B]
+// "piece_fused" (option): 0 K1 + K2 (two launches), 1 the fused launch for eager calls (captured calls
+// always take K1 + K2: the fused tags are per call, a graph would replay one tag); "fused_walkers":
+// walker blocks in front of the unmask blocks (each one: 16 segment walks at a time).
+WsOpt ws_piece_fused{0};
+WsOpt ws_fused_walkers{64};
+
+size_t ws_fused_bytes(u64 span, u32 nseg, u32 max_frames) {
+    const u64 npieces = (span + 15) / (1ull << PIECE_SHIFT) + 2;
+    return 64 + npieces * 16 + (((size_t)nseg * 8 + 15) & ~(size_t)15) + (size_t)nseg * max_frames * 16 + 16;
+}
+
+bool ws_fused_enabled() { return ws_piece_fused != 0; }
+
+int ws_launch_piece_fused(const WsLaunch& L, u64 lo, u64 hi, unsigned char* fb, u32 gen, int* advice, u32 g0,
+                          bool* fallback_needed) {
+    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
+    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
+    PieceWs P;
+    P.npieces = piece_count(lo_org, hi_org);
+    *fallback_needed = P.npieces == 0;
+    if (!P.npieces) return ws_set_msg("fused decode: no pieces");
+    P.pbase = lo_org >> PIECE_SHIFT;
+    P.c_lo = lo_org >> 4;
+    P.c_hi = (hi_org + 15) >> 4;
+    P.disorder = nullptr;
+    P.nonuni = nullptr;
+    P.nwork = nullptr;
+    P.segr = nullptr;
+    P.ptr = reinterpret_cast<u64*>(fb + 64);
+    size_t b = 64 + P.npieces * 16;
+    const u64* done = reinterpret_cast<const u64*>(fb + b);
+    b += ((size_t)L.nseg * 8 + 15) & ~(size_t)15;
+    P.items = reinterpret_cast<u32x4*>(fb + b);
+    size_t tslot = 0;
+    int rc;
+    const int timing = ws_k2_timing;
+    if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
+    const u32 wshift = piece_wshift(P.npieces);
+    const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
+    const u64 grid = ppw << wshift;
+    const int nw_opt = ws_fused_walkers;
+    const u64 nw_max = ((u64)L.nseg + (PIECE_T / WALK_G) - 1) / (PIECE_T / WALK_G);   // >= one segment per group
+    const u32 nwb = (u32)((u64)(nw_opt < 1 ? 1 : nw_opt) < nw_max ? (u64)(nw_opt < 1 ? 1 : nw_opt) : nw_max);
+    if (grid + nwb > 0x7FFFFFFFull) return ws_set_msg("fused decode: batch too large for one launch");
+    WalkArgs W;
+    W.buf = L.buf; W.seg_off = L.seg_off; W.seg_len = L.seg_len; W.nseg = L.nseg; W.max_frames = L.max_frames;
+    W.desc_base = L.desc_base; W.desc = L.desc; W.res = L.res; W.items = P.items; W.ptr = P.ptr; W.nwork = nullptr;
+    W.segr = nullptr; W.disorder = nullptr; W.gen = gen; W.pbase = P.pbase; W.lo = lo; W.hi = hi;
+    W.g0 = g0 < (1u << 31) ? g0 : 0u;
+    UnmaskArgs A = unmask_args(L, P, gen, advice, wshift, ppw);
+    A.done = done;
+    A.head = reinterpret_cast<FusedHead*>(fb);
+    A.nwb = nwb;
+    hipLaunchKernelGGL(ws_piece_fused_kernel, dim3((u32)(grid + nwb)), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, W, A);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return ws_set_err("ws_piece_fused_kernel launch", e);
+    return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
 }
