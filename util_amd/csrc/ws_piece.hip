@@ -39,25 +39,23 @@ static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's
 
 // ---- hand-off helpers of the fused form (ws_piece_fused_kernel below). Walker waves publish with
 // write-through (sc1) stores, wait for them (vmcnt(0)), then store a generation-tagged word; the
-// unmask waves poll tagged words with scalar loads that bypass the scalar cache (glc) and read the
-// published items with sc1 vector loads (L1 bypass): MI355X_MICROARCH.md, "Workgroup dispatch, XCD
-// placement & inter-workgroup visibility", hand-off form of row 1 (hipMalloc memory).
+// unmask waves poll tagged words and read the published items with sc1 vector loads (L1 bypass):
+// MI355X_MICROARCH.md, "Workgroup dispatch, XCD placement & inter-workgroup visibility", hand-off
+// form of row 1 (hipMalloc memory).
+// (compiler-emitted 8-B atomic accesses, global_load/store_dwordx2 sc1: inline-asm stores would
+// escape the compiler's hazard handling — a VALU write to a store's data registers right after the
+// store issued tore 16-B items on the GPU — and inline-asm loads its wait-count tracking)
 __device__ __forceinline__ void st16_sc1(gu32x4* p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    u64* q = reinterpret_cast<u64*>(reinterpret_cast<uintptr_t>(p));
+    __hip_atomic_store(q, (u64)v.x | ((u64)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (u64)v.z | ((u64)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ u32x4 ld16_sc1(const gu32x4* p) {
+    u64* q = reinterpret_cast<u64*>(reinterpret_cast<uintptr_t>(p));
+    const u64 a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ u32x4 sld16_glc(const void* p) {
-    u32x4 v;
-    asm volatile("s_load_dwordx4 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ u64 sld8_glc(const void* p) {
-    u64 v;
-    asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    v.x = (u32)a; v.y = (u32)(a >> 32); v.z = (u32)b; v.w = (u32)(b >> 32);
     return v;
 }
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -76,7 +74,9 @@ __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
 // of the batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the
 // batch unordered, and its pointers are clipped here). Classic table: one u64 s << 32 | k per
 // piece. Fused table: 16 B {s, tag, k, tag} per piece, stored write-through (each 8-B half
-// carries the call's tag, so a half read before the store lands is never taken as current).
+// carries the call's tag, so a half read before the store lands is never taken as current); k's
+// bit 31 (FUSED_NOFRAME) marks a pointer that is not a frame's (gap before the segment, tail):
+// a frame pointer is stored only after the items up to its frame have landed.
 template <bool FUSED>
 __device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u32 tag) {
     u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
@@ -90,6 +90,8 @@ __device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo,
         }
     }
 }
+
+#define FUSED_NOFRAME 0x80000000u
 
 // What one segment walk needs (K1, and the walker blocks of the fused kernel).
 struct WalkArgs {
@@ -135,7 +137,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
     const u64 ibase = (u64)sc * A.max_frames;
     const u64 sorg = so + lead0;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(A.buf + so);
-    if (active && gl == 0) put_ptrs<FUSED>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, A.gen);
+    if (!FUSED && active && gl == 0) put_ptrs<false>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, 0);
     // g0: the stride guess of the first step (the host's hint, 0 = none): lane k parses off + k*g0
     // at once; lane 0's frame is always the true first one, so a wrong guess costs nothing but
     // its loads (code 1 at lane 0 takes the true length)
@@ -180,8 +182,12 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         if (gl < ntake) {                                                   // consumed frames, in parallel
             put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + gl), p0, h.masked ? fe : p0,
                             rotl32(h.key, 8u * (u32)(p0 & 3)));
-            put_ptrs<FUSED>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, A.gen);
+            if (!FUSED) put_ptrs<false>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, 0);
             if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + gl, so + pos, h);
+        }
+        if (FUSED) {                                                        // items out before their pointers
+            wait_stores();
+            if (gl < ntake) put_ptrs<true>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, A.gen);
         }
         const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
         if (ntake) walked_end = fe_last;
@@ -211,7 +217,12 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         active = false;
         if (gl == 0) {
             const u32 cnt = nf + extra;
-            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt, A.gen);   // pieces starting in the tail
+            const u32 nofr = FUSED ? FUSED_NOFRAME : 0u;
+            if (FUSED) {                                                    // the gap before the segment
+                wait_stores();
+                put_ptrs<true>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, nofr, A.gen);
+            }
+            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt | nofr, A.gen);   // pieces starting in the tail
             if (sc == A.nseg - 1)
                 put_ptrs<FUSED>(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, A.gen);
             ws_store_res(A.res + sc, off, nf, status);
@@ -281,10 +292,16 @@ struct FusedHead {
 static_assert(sizeof(FusedHead) == 64, "fused head");
 #define FUSED_SPINS (1u << 16)    // polls (s_sleep 2 each) before a wave gives up waiting (tens of ms)
 
-// poll a tagged word (scalar, wave-uniform): true when current, false when the wait gave up
+// Polls are vector loads with sc1 (L1 bypass; MI355X_MICROARCH.md: scalar loads go through the
+// scalar cache, which another CU's stores never refresh), one lane's word read by every lane.
+__device__ __forceinline__ u64 poll8(const u64* p) {
+    return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// poll segment s's tagged item count (wave-uniform): true when current, false when the wait gave up
 __device__ __forceinline__ bool poll_done(const u64* done, u32 s, u32 gen, u32& cnt) {
     for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
-        const u64 d = sld8_glc(done + s);
+        const u64 d = poll8(done + s);
         if ((u32)(d >> 32) == gen) {
             cnt = (u32)d;
             return true;
@@ -315,6 +332,14 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(A.buf) & ~(uintptr_t)15);
     const u64 c_lo = A.c_lo, c_hi = A.c_hi;
     // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
+    // fused: the first poll (lane 0 the order verdict, lanes 1-2 this piece's pointer, 3-4 the
+    // next one's) goes out before the payload loads, so its answer does not queue behind them
+    const u64* const pt = reinterpret_cast<const u64*>(A.ptr);
+    const u64 pnext = pidx + 1 < A.npieces ? pidx + 1 : pidx;
+    const u64* const paddr = lane == 0 ? &A.head->verdict : (lane < 3 ? pt + 2 * pidx + (lane - 1)
+                                                                      : pt + 2 * pnext + (lane & 1 ? 0 : 1));
+    u64 pw0 = 0;
+    if (FUSED) pw0 = poll8(lane < 5 ? paddr : pt + 2 * pidx);
     u32x4 v[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) {
@@ -332,28 +357,33 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
         // the order verdict and this piece's pointer (the next piece's too, if already current:
         // it bounds the first item load, as below)
         const u32 gen = A.gen;
-        const u32x4* pt = reinterpret_cast<const u32x4*>(A.ptr);
-        u32x4 pv = {0, 0, 0, 0};
         failed = true;
+        u64 w = pw0;
         for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
-            const u64 vd = sld8_glc(&A.head->verdict);
-            pv = sld16_glc(pt + pidx);
-            if ((u32)(vd >> 1) == gen && ((vd & 1) || (pv.y == gen && pv.w == gen))) {
+            const u64 vd = (u64)__builtin_amdgcn_readlane((int)(u32)w, 0) | ((u64)(u32)__builtin_amdgcn_readlane((int)(w >> 32), 0) << 32);
+            const u32 t1 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 1);
+            const u32 t2 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 2);
+            if ((u32)(vd >> 1) == gen && ((vd & 1) || (t1 == gen && t2 == gen))) {
                 failed = false;
                 ok = !(vd & 1);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
+            w = poll8(lane < 5 ? paddr : pt + 2 * pidx);
         }
-        if (ok && pvalid && pv.x != 0xFFFFFFFFu) {
-            s = pv.x;
-            k = pv.z;
-            if (pidx + 1 < A.npieces) {
-                const u32x4 pn = sld16_glc(pt + pidx + 1);
-                if (pn.y == gen && pn.w == gen && pn.x == s && pn.z >= k && pn.z - k < 16u) {
-                    step = pn.z - k + 1;
-                    exact = true;
-                }
+        // this piece: lanes 1-2 = {s, tag}, {k, tag}; the next one: lanes 3-4
+        const u32 ps = (u32)__builtin_amdgcn_readlane((int)(u32)w, 1), pk = (u32)__builtin_amdgcn_readlane((int)(u32)w, 2);
+        if (ok && pvalid && ps != 0xFFFFFFFFu) {
+            s = ps;
+            k = pk & ~FUSED_NOFRAME;
+            // both pointers frame pointers of one segment: the items [k, k'] have landed and are
+            // all this piece needs — no wait for the segment's count
+            const u32 ns = (u32)__builtin_amdgcn_readlane((int)(u32)w, 3), nk = (u32)__builtin_amdgcn_readlane((int)(u32)w, 4);
+            const u32 n1 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 3), n2 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 4);
+            if (pnext != pidx && n1 == gen && n2 == gen && ns == s && !(pk & FUSED_NOFRAME) && !(nk & FUSED_NOFRAME) &&
+                nk >= k && nk - k < 16u) {
+                step = nk - k + 1;
+                exact = true;
             }
         }
     } else {
@@ -405,9 +435,12 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
         }
         if (!first && slo >= r1) break;                                     // the next segment starts past us
         first = false;
-        if (FUSED && !poll_done(A.done, s, A.gen, cnt)) {
-            failed = true;
-            break;
+        if (FUSED) {
+            if (exact) cnt = k + step;                                      // items [k, k + step) landed
+            else if (!poll_done(A.done, s, A.gen, cnt)) {
+                failed = true;
+                break;
+            }
         }
         {
             // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
@@ -491,7 +524,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
         if (FUSED) {
             go = false;
             for (u32 spins = 0; spins < FUSED_SPINS && !go; ++spins) {
-                go = (u32)sld8_glc(&A.head->donew) == A.gen;
+                go = (u32)poll8(reinterpret_cast<const u64*>(&A.head->donew)) == A.gen;
                 if (!go) __builtin_amdgcn_s_sleep(2);
             }
         }
@@ -532,7 +565,7 @@ __device__ __forceinline__ u32 task_seg(u64 t, u32 s1, u32 nseg) {
 // them; (3) the last walker block to finish writes the host's stride hint. Blocks [nwb, grid) are
 // K2's unmask blocks: each issues its payload loads first, then polls its piece's pointer and
 // segment counts (walkers run ahead: dispatched first, they never wait on anything).
-__global__ __launch_bounds__(PIECE_T) void ws_piece_fused_kernel(WalkArgs W, UnmaskArgs A) {
+__global__ __launch_bounds__(PIECE_T, 6) void ws_piece_fused_kernel(WalkArgs W, UnmaskArgs A) {
     if (blockIdx.x >= A.nwb) {
         unmask_piece<1, 0, true>(A, blockIdx.x - A.nwb);
         return;
@@ -790,6 +823,10 @@ bool ws_fused_enabled() { return ws_piece_fused != 0; }
 
 int ws_launch_piece_fused(const WsLaunch& L, u64 lo, u64 hi, unsigned char* fb, u32 gen, int* advice, u32 g0,
                           bool* fallback_needed) {
+    if (L.max_frames >= FUSED_NOFRAME) {                                 // k's flag bit must be free
+        *fallback_needed = true;
+        return ws_set_msg("fused decode: max_frames >= 2^31");
+    }
     const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
     const u64 lo_org = lo + lead0, hi_org = hi + lead0;
     PieceWs P;
