@@ -250,7 +250,13 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
     const u64 r0 = (((u64)pb << ENC_SHIFT) + (u64)wv * (64 * ENC_U * 16));  // origin-relative
     const u64 r1 = r0 + 64 * ENC_U * 16;
     const u32 first = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + pb));
+    // the next piece's first frame: the frames that touch this piece are exactly [first, that
+    // one] (it holds the next piece's first byte), so the first record load takes only those —
+    // with pieces dealt round-robin over the XCDs, 16 records per wave would pull each record
+    // line into most of the 8 L2s
+    const u32 nxt = pb + 1 < npieces ? *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(ptr + pb + 1)) : ENC_NONE;
     if (first == ENC_NONE) return;
+    const bool exact = nxt != ENC_NONE && nxt >= first && nxt - first < 16u;
     // chunk state: fast = one payload source for the whole chunk
     u64 fsrc[ENC_U];
     u32 fkey[ENC_U];
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
     for (int u = 0; u < ENC_U; ++u) { kind[u] = 0; fsrc[u] = 0; fkey[u] = 0; }
     // records load `step` at a time: 16 first (a 4 KiB wave range rarely needs more), 64 after
     // that — 64 lanes loading would fetch 2 KiB of records per wave, into every XCD's L2
-    for (u32 k = first, step = 16; k < n;) {
+    for (u32 k = first, step = exact ? nxt - first + 1 : 16; k < n;) {
         const u32 j = k + lane;
         const bool valid = j < n && lane < step;
         EncFrame e = {};
@@ -312,7 +318,7 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
             if (mine && enc_edge_eligible(e, nx, j, n, lead0, out_lo, out_hi))
                 enc_edge_store(src, base, e, nx, nxt, lead0, r0, r1);
         }
-        if (nlim < step) break;
+        if (nlim < step || exact) break;
         k += step;
         step = 64;
     }
