@@ -231,7 +231,9 @@ WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long va
  * stored nothing — never expected; reading it synchronizes the devices), "workspace_bytes" (device bytes held
  * in workspace slots), and of the calling process's most recent call: "stream_rw_chunks"
  * (chunks of a long stream written from the chunk-parallel walk's records),
- * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront); with the option
+ * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront), "stream_skips" (eager raw-stream
+ * calls since load that skipped the pass rounds because the previous chunk walk on the stream saw
+ * lengths that keep changing); with the option
  * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece
  * path's unmask launches since the option was set, from HIP events around each launch;
  * reading them waits for those launches). Returns 0, or -1 for an unknown name. */

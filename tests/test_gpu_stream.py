@@ -231,3 +231,22 @@ def test_stream_state_survives_mixed_calls(dev):
         W.batch_decode_device(d, so_t, sl_t, 64, desc, res)
         torch.cuda.synchronize()
         assert int(res.cpu().numpy().view(W.SEGRES_DTYPE)[0]["n_frames"]) == 64
+
+
+def test_stream_skips_rounds_while_lengths_keep_changing(dev):
+    """eager calls on one stream: after a chunk walk whose sample saw lengths that keep changing,
+    the next call skips the pass rounds (its walk starts at 0); a uniform stream then seen by
+    that walk sends the call after it back to the rounds. Every call bit-exact vs the oracle."""
+    mixed, *_ = wsynth.make_batch(1500, wsynth.PLEN_MIX3, 0, 0, 46)
+    mixed2, *_ = wsynth.make_batch(1400, wsynth.PLEN_MIX3, 0, 0, 47)
+    uni, *_ = wsynth.make_batch(20000, 0, 4096, 0, 3)
+    W.set_option("stream_rw", 1)
+    # (stream, skips the rounds); the first call may follow another test's call on this stream
+    seq = [(mixed, None), (mixed, True), (mixed2[:len(mixed2) - 777], True), (uni, True), (uni, False),
+           (mixed, False), (mixed2, True), (mixed2, True)]
+    for i, (w, want) in enumerate(seq):
+        n0 = W.get_stat("stream_skips")
+        run(dev, w, 1 << 14, shift=5 if i == 6 else 0)
+        skipped = W.get_stat("stream_skips") == n0 + 1
+        if want is not None:
+            assert skipped == want, (i, skipped)

@@ -39,7 +39,7 @@ extern std::atomic<unsigned long long> ws_stat_fused_calls;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
-extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks;
+extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -135,6 +135,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     }
     if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks.load();
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
+    else if (!strcmp(name, "stream_skips")) *value = ws_stat_stream_skips.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
     else if (!strcmp(name, "fused_calls")) *value = ws_stat_fused_calls.load();
     else if (!strcmp(name, "fused_fails")) return fused_fails(value);

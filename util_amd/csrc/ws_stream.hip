@@ -91,7 +91,8 @@ struct SdState {
 static_assert(sizeof(SdState) <= 128, "stream state");
 struct SdMirror {                    // pinned host copy of the state after a resolve (eager calls)
     u64 P, g;
-    u32 nf, phase, gen, pad;
+    u32 nf, phase, gen;
+    u32 walk_hint;                   // the last chunk walk's sample: lengths kept changing (next call: no rounds)
 };
 
 // reset of a state left dirty by a call that failed between its launches (rare)
@@ -153,6 +154,7 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned 
 struct SwOut {            // where a stream_walk stopped: the next frame, its index, 1 if the walk ended
     u64 next;
     u32 nf, ended;
+    u32 steps;            // header rounds the walk took (a run of equal frames takes one per 64)
 };
 __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ buf, u64 len, u64 P0, u64 g0, u32 nf0,
                                             u64 end, bool last, u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
@@ -165,7 +167,9 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
     u32 nf = nf0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
     bool at_bnd = false;
+    u32 steps = 0;
     for (;;) {
+        ++steps;
         const u64 pos = off + (u64)lane * g;
         const bool cand = lane == 0 || g > 0;
         const bool eval = cand && pos < len;
@@ -227,6 +231,7 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
     r.next = off;
     r.nf = nf;
     r.ended = at_bnd ? 0u : 1u;
+    r.steps = steps;
     if (!last && (at_bnd || !out)) return r;
     const u32 cnt = nf + extra;
     for (u64 p = ((walked_end + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + lane;
@@ -716,18 +721,34 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u64 cmin, u64 cmax, u32 nchunks_cap, u64 cand_cap, u64 stg_cap,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
-                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
+                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
+                                                        int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
+                                                        SdMirror* __restrict__ mirror) {
     const u32 lane = threadIdx.x;
-    if (sd->phase == SD_DONE) {                                              // the passes finished it
+    if (!fresh && sd->phase == SD_DONE) {                                    // the passes finished it
         if (lane == 0) plan->active = 0;
         return;
     }
-    const u64 P = sd->P;
-    const u32 nf = sd->nf;
+    // fresh: no pass rounds ran (the previous chunk walk on this stream saw lengths that keep
+    // changing): the walk starts at (0, 0), and this kernel does the first round's chores — the
+    // unmask's segment pair and gate word, and the pieces before the first frame
+    const u64 P = fresh ? 0 : sd->P;
+    const u32 nf = fresh ? 0 : sd->nf;
+    if (fresh && lane == 0) {
+        seg[0] = 0;
+        seg[1] = len;
+        *disorder = 0;
+        if (reinterpret_cast<uintptr_t>(buf) & 15) ptr[0] = 0;               // piece 0 starts before the frame
+    }
     // the sample (a walk that ends in it finishes the stream: `out` given)
     const u64 send = len - P > RW_SAMPLE ? P + RW_SAMPLE : len;
-    const SwOut o = stream_walk(buf, len, P, sd->g, nf, send, false, max_frames, desc, items, ptr, pend, nwork, res,
-                                lane, plan->sample_out);
+    const SwOut o = stream_walk(buf, len, P, fresh ? 0 : sd->g, nf, send, false, max_frames, desc, items, ptr, pend,
+                                nwork, res, lane, plan->sample_out);
+    // the next call on this stream may skip the pass rounds while the sample's lengths keep
+    // changing (>= 8 frames, fewer than 4 per header round; a stream of runs or equal frames: rounds)
+    if (mirror && lane == 0)
+        __hip_atomic_store(&mirror->walk_hint, !o.ended && o.nf - nf >= 8 && (u64)o.steps * 4 > (u64)(o.nf - nf) ? 1u : 0u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (o.ended) {
         if (lane == 0) plan->active = 0;
         return;
@@ -1073,6 +1094,7 @@ WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
+std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
 
 // scratch for the chunk-parallel walk: the call's slot's auxiliary workspace (device
@@ -1294,7 +1316,8 @@ static RwDevLayout rw_dev_layout(u64 len) {
 
 static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, WebsocketFrameDesc_t* d_desc,
                           const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st, const SdState* sd,
-                          unsigned char* w, const RwDevLayout& L) {
+                          unsigned char* w, const RwDevLayout& L, int fresh = 0, u64* d_seg = nullptr,
+                          SdMirror* mirror = nullptr) {
     RwPlan* plan = reinterpret_cast<RwPlan*>(w + L.o_plan);
     u32* nrec = reinterpret_cast<u32*>(w + L.o_nrec);
     unsigned long long* dx = reinterpret_cast<unsigned long long*>(w + L.o_dx);
@@ -1308,7 +1331,8 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
-                       (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res);
+                       (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
+                       fresh, d_seg, Pw.disorder, mirror);
     // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
     hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        cand, nrec, 0u, (const RwPlan*)plan);
@@ -1444,6 +1468,17 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
             __builtin_ia32_pause();
         }
     };
+    // the previous chunk walk on this stream saw lengths that keep changing: no pass rounds and
+    // no wait for their published state — the device walk starts at 0 (its plan kernel re-checks
+    // the lengths on its sample and tells the next call)
+    if (rw_opt == 1 && __atomic_load_n(&hm->walk_hint, __ATOMIC_RELAXED) == 1) {
+        ++ws_stat_stream_skips;
+        *A.state_ok = true;
+        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
+                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 1, d_seg, dm)))
+            return rc;
+        return ws_launch_piece_unmask(L, Pw, gen);
+    }
     u32 tag = ws_next_gen();
     if ((rc = rounds(1, false, tag)) || (rc = published(tag))) return rc;
     while (hm->phase == SD_PASSES) {
@@ -1456,7 +1491,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         const u32 nf = hm->nf;
         if (len - P >= RW_MIN && rw_opt == 1) {                              // lengths keep changing:
             if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,    // the device walks
-                                     reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL)))
+                                     reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 0, d_seg, dm)))
                 return rc;
         } else if (len - P >= RW_MIN) {                                      // ... the host follows
             if ((rc = rw_walk(slot, d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
