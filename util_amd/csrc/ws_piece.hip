@@ -146,9 +146,52 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
     int status = WEBSOCKET_SEG_OK;
     bool nonu = false;                       // frames of another length than the first, or an error stop
     const u64 gmask = (1ull << G) - 1;
+    // ALPHABET SPECULATION (lengths that keep changing, e.g. cfg3): once a step ends after one
+    // frame of a new length, the lanes speculate over the lengths seen so far (L0..L2, na of them)
+    // instead of one stride: lane 0 parses the frame at off, lanes 1..na the frame after it for
+    // each length, the next lanes the frame after that for each pair (and, with two lengths, each
+    // triple) — 13 lanes cover three frames (15 cover four) while the lengths stay in the
+    // alphabet, where stride lanes confirm one or two. A chain of three equal lengths goes back
+    // to stride speculation.
+    bool alpha = false;
+    u32 L0 = 0, L1 = 0, L2 = 0, na = 0, rep = 0;
+    // (selects only: an indexed form becomes a scratch array)
+    auto add_len = [&](u32 x) {
+        const bool add = x != 0 && x != L0 && !(na > 1 && x == L1) && !(na > 2 && x == L2);
+        const u32 at = na < 3 ? na : rep;                                   // fill, then replace round-robin
+        L0 = add && at == 0 ? x : L0;
+        L1 = add && at == 1 ? x : L1;
+        L2 = add && at == 2 ? x : L2;
+        rep = add && na == 3 ? (rep == 2 ? 0u : rep + 1) : rep;
+        na = add && na < 3 ? na + 1 : na;
+    };
+    auto len_at = [&](u32 i) -> u64 { return (u64)(i == 0 ? L0 : (i == 1 ? L1 : L2)); };
     while (__ballot(active)) {
-        const u64 pos = off + (u64)gl * g;                                  // candidate frame offset
-        const bool cand = active && (gl == 0 || g > 0);
+        // this lane's candidate: its frame offset and its depth in the chain
+        u64 pos = off;
+        u32 depth = 0;
+        bool cand = active;
+        if (!alpha) {
+            pos = off + (u64)gl * g;
+            depth = gl;
+            cand = active && (gl == 0 || g > 0);
+        } else if (gl >= 1) {
+            const u32 q = gl - 1;
+            if (q < na) {
+                depth = 1;
+                pos = off + len_at(q);
+            } else if (q - na < na * na) {
+                const u32 r = q - na;
+                depth = 2;
+                pos = off + len_at(r / na) + len_at(r % na);
+            } else if (na == 2 && q - 6 < 8) {
+                const u32 r = q - 6;
+                depth = 3;
+                pos = off + len_at(r >> 2) + len_at((r >> 1) & 1) + len_at(r & 1);
+            } else {
+                cand = false;
+            }
+        }
         const bool eval = cand && pos < sl;
         const uintptr_t pa = seg + (eval ? pos : 0);
         const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
@@ -157,53 +200,97 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         ws_hdr_from32(x0, x1, (u32)(pa & 15), h0, h1);
         const WsHdr h = ws_parse(h0, h1, eval ? sl - pos : 0);
         // per-lane outcome in the reactor loop's order (net_reactor.c:515-526):
-        //   0 consumed, chain continues   1 consumed, length != g: step ends
+        //   0 consumed, chain continues   1 consumed, length != g: step ends (stride lanes)
         //   2 consumed, walk ends (ret <= 0)   3 not consumed, walk ends
         u32 code = 3;
         int st = WEBSOCKET_SEG_OK;
         if (cand) {
             if (pos >= sl) code = 3;
-            else if (nf + gl >= A.max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
+            else if (nf + depth >= A.max_frames) { code = 3; st = WEBSOCKET_SEG_MAX_FRAMES; }
             else if (sl - pos < 2) code = 3;                                 // websocketframe.c:121
             else if (h.kind == WS_PARSE_INCOMPLETE) code = 3;
             else if (h.kind == WS_PARSE_WRAP) { code = 3; st = WEBSOCKET_SEG_ERR_LEN_WRAP; }
             else if (h.ret <= 0) { code = 2; st = h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
-            else code = (u64)(u32)h.ret == g ? 0u : 1u;
+            else code = alpha || (u64)(u32)h.ret == g ? 0u : 1u;
         }
-        const u64 stop = (__ballot(code != 0) >> gb) & gmask;
-        const u32 mm = stop ? (u32)__builtin_ctzll(stop) : G;              // first non-continuing lane
-        const u32 src = gb + (mm < G ? mm : G - 1);
-        const u32 code_m = mm < G ? (u32)__shfl((int)code, (int)src) : 0u;
-        const int ret_m = __shfl(h.ret, (int)src);
-        const int st_m = __shfl(st, (int)src);
+        // the chain: mm = frames before the stopping one (G: none stops), the stopping lane's code,
+        // and (alpha) the chain's lanes by depth
+        u32 mm, code_m, lm = 0;
+        u32 cl1 = 0, cl2 = 0, cl3 = 0;
+        if (!alpha) {
+            const u64 stop = (__ballot(code != 0) >> gb) & gmask;
+            mm = stop ? (u32)__builtin_ctzll(stop) : G;                      // first non-continuing lane
+            lm = mm < G ? mm : G - 1;
+            code_m = mm < G ? (u32)__shfl((int)code, (int)(gb + lm)) : 0u;
+        } else {
+            // walk the tree: depth t's lane continues to the child for its length, if any
+            const u32 maxd = na == 2 ? 3u : 2u;
+            u32 lc = 0, qi = 0, t = 0;
+            code_m = 1;                                                     // "stops after a consumed frame"
+            for (;; ++t) {
+                const u32 c = (u32)__shfl((int)code, (int)(gb + lc));
+                if (c != 0) { code_m = c; break; }                          // 2 or 3: the walk ends here
+                const u32 r = (u32)__shfl(h.ret, (int)(gb + lc));
+                const u32 idx = r == L0 ? 0u : (na > 1 && r == L1 ? 1u : (na > 2 && r == L2 ? 2u : 3u));
+                if (idx == 3u || t == maxd) break;                          // next length unknown: round ends
+                qi = t == 0 ? idx : qi * na + idx;
+                lc = t == 0 ? 1 + qi : (t == 1 ? 1 + na + qi : 1 + na + na * na + qi);
+                if (t == 0) cl1 = lc; else if (t == 1) cl2 = lc; else cl3 = lc;
+            }
+            mm = t;
+            lm = lc;
+        }
+        const int ret_m = __shfl(h.ret, (int)(gb + lm));
+        const int st_m = __shfl(st, (int)(gb + lm));
         const u32 ntake = active ? mm + ((code_m == 1 || code_m == 2) ? 1u : 0u) : 0u;
+        // this lane's frame is consumed: its index in the segment is nf + depth
+        const bool mine = alpha ? depth < ntake && gl == (depth == 0 ? 0u : (depth == 1 ? cl1 : (depth == 2 ? cl2 : cl3)))
+                                : gl < ntake;
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
-        if (gl < ntake) {                                                   // consumed frames, in parallel
-            put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + gl), p0, h.masked ? fe : p0,
+        if (mine) {                                                         // consumed frames, in parallel
+            put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
                             rotl32(h.key, 8u * (u32)(p0 & 3)));
-            if (!FUSED) put_ptrs<false>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, 0);
-            if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + gl, so + pos, h);
+            if (!FUSED) put_ptrs<false>(A.ptr, A.pbase, pend, fo, fe, sc, nf + depth, 0);
+            if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + depth, so + pos, h);
         }
         if (FUSED) {                                                        // items out before their pointers
             wait_stores();
-            if (gl < ntake) put_ptrs<true>(A.ptr, A.pbase, pend, fo, fe, sc, nf + gl, A.gen);
+            if (mine) put_ptrs<true>(A.ptr, A.pbase, pend, fo, fe, sc, nf + depth, A.gen);
         }
-        const u64 fe_last = __shfl(fe, (int)(gb + (ntake ? ntake - 1 : 0)));
+        // the last consumed frame's lane: the stopping lane if it consumed, else the one before it
+        const u32 llast = (code_m == 1 || code_m == 2 || mm == G) ? lm
+                          : (alpha ? (mm == 1 ? 0u : (mm == 2 ? cl1 : (mm == 3 ? cl2 : cl3))) : (mm ? mm - 1 : 0u));
+        const u64 fe_last = __shfl(fe, (int)(gb + llast));
+        const u64 pos_m = __shfl(pos, (int)(gb + lm));
         if (ntake) walked_end = fe_last;
         if (!active) continue;
-        if (mm == G) {                                                      // the whole step continued
+        if (!alpha && mm == G) {                                            // the whole step continued
             nf += G;
             off += G * g;
+            add_len((u32)g);
             continue;
         }
-        const u64 pos_m = off + (u64)mm * g;
         nf += mm;
-        if (code_m == 1) {                                                  // consumed, new stride
-            if (nf) nonu = true;
+        if (code_m == 1) {                                                  // consumed, next length unknown
+            if (!alpha) {
+                if (nf) nonu = true;
+                if (mm) add_len((u32)g);
+                add_len((u32)ret_m);
+                // a step that confirmed one frame of a new length: lengths keep changing
+                alpha = mm == 0 && nf > 0 && na >= 2;
+                g = (u32)ret_m;
+            } else {
+                // a chain of three or more equal lengths: back to stride speculation
+                const u32 r0 = (u32)__shfl(h.ret, (int)gb);
+                if (mm >= 2 && r0 == (u32)ret_m && (u32)__shfl(h.ret, (int)(gb + cl1)) == r0) {
+                    alpha = false;
+                    g = (u32)ret_m;
+                }
+                add_len((u32)ret_m);
+            }
             nf += 1;
             off = pos_m + (u32)ret_m;
-            g = (u32)ret_m;
             continue;
         }
         off = pos_m;
