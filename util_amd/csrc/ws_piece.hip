@@ -265,14 +265,15 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         const u64 pos_m = __shfl(pos, (int)(gb + lm));
         if (ntake) walked_end = fe_last;
         if (!active) continue;
+        // (a walk whose next frame would start at or past the segment's end stops now: the next
+        // round's lane 0 would find pos >= sl and stop there with status OK)
         if (!alpha && mm == G) {                                            // the whole step continued
             nf += G;
             off += G * g;
             add_len((u32)g);
-            continue;
-        }
-        nf += mm;
-        if (code_m == 1) {                                                  // consumed, next length unknown
+            if (off < sl) continue;
+        } else if (code_m == 1) {                                           // consumed, next length unknown
+            nf += mm;
             if (!alpha) {
                 if (nf) nonu = true;
                 if (mm) add_len((u32)g);
@@ -291,16 +292,18 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             }
             nf += 1;
             off = pos_m + (u32)ret_m;
-            continue;
+            if (off < sl) continue;
+        } else {
+            nf += mm;
+            off = pos_m;
+            if (code_m == 2) {
+                if (ret_m != 0) nf += 1;                                    // ret < 0 keeps its descriptor
+                else extra = 1;                                             // ret == 0: unmasked, not counted
+                nonu = true;
+            }
+            status = st_m;
+            if (st_m == WEBSOCKET_SEG_ERR_LEN_WRAP) nonu = true;
         }
-        off = pos_m;
-        if (code_m == 2) {
-            if (ret_m != 0) nf += 1;                                        // ret < 0 keeps its descriptor
-            else extra = 1;                                                 // ret == 0: unmasked, not counted
-            nonu = true;
-        }
-        status = st_m;
-        if (st_m == WEBSOCKET_SEG_ERR_LEN_WRAP) nonu = true;
         active = false;
         if (gl == 0) {
             const u32 cnt = nf + extra;
