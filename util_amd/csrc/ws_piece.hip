@@ -77,10 +77,15 @@ __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
 // carries the call's tag, so a half read before the store lands is never taken as current); k's
 // bit 31 (FUSED_NOFRAME) marks a pointer that is not a frame's (gap before the segment, tail):
 // a frame pointer is stored only after the items up to its frame have landed.
+// (start, stride: the lanes of a group write one range together, lane j the pieces j, j + stride, ...)
+__device__ __forceinline__ u64 first_piece(u64 lo, u64 pbase) {
+    const u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
+    return p > pbase ? p : pbase;
+}
 template <bool FUSED>
-__device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u32 tag) {
-    u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
-    for (p = p > pbase ? p : pbase; (p << PIECE_SHIFT) < hi && p < pend; ++p) {
+__device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u32 tag,
+                                         u64 start = 0, u64 stride = 1) {
+    for (u64 p = first_piece(lo, pbase) + start; (p << PIECE_SHIFT) < hi && p < pend; p += stride) {
         if (FUSED) {
             u32x4 q;
             q.x = s; q.y = tag; q.z = k; q.w = tag;
@@ -121,6 +126,7 @@ struct WalkArgs {
 // return lane gl == 0 of the group holds its item count and whether its frames were not all of
 // one length (or it stopped on an error).
 #define WALK_G 16
+#define WALK_PTR_OWN 4    // piece pointers of its frame a lane writes alone
 template <bool FUSED>
 __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active, u32 lane, u32& cnt_out,
                                            bool& nonu_out) {
@@ -137,7 +143,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
     const u64 ibase = (u64)sc * A.max_frames;
     const u64 sorg = so + lead0;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(A.buf + so);
-    if (!FUSED && active && gl == 0) put_ptrs<false>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, 0);
+    if (!FUSED && active) put_ptrs<false>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, 0, gl, G);
     // g0: the stride guess of the first step (the host's hint, 0 = none): lane k parses off + k*g0
     // at once; lane 0's frame is always the true first one, so a wrong guess costs nothing but
     // its loads (code 1 at lane 0 takes the true length)
@@ -251,12 +257,28 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         if (mine) {                                                         // consumed frames, in parallel
             put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
                             rotl32(h.key, 8u * (u32)(p0 & 3)));
-            if (!FUSED) put_ptrs<false>(A.ptr, A.pbase, pend, fo, fe, sc, nf + depth, 0);
             if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + depth, so + pos, h);
         }
-        if (FUSED) {                                                        // items out before their pointers
-            wait_stores();
-            if (mine) put_ptrs<true>(A.ptr, A.pbase, pend, fo, fe, sc, nf + depth, A.gen);
+        if (FUSED) wait_stores();                                           // items out before their pointers
+        // the pieces whose first byte lies in a consumed frame point at it: a lane writes its frame's
+        // first WALK_PTR_OWN pieces; a longer frame's rest the group's 16 lanes write together
+        // (one lane alone would take milliseconds over a multi-GiB frame)
+        const u64 pf = first_piece(fo, A.pbase);
+        const u64 phi = (fe + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;   // pieces [pf, phi) start in [fo, fe)
+        const u64 pl = phi < pend ? phi : pend;
+        if (mine) {
+            const u64 hown = pf + WALK_PTR_OWN < pl ? (pf + WALK_PTR_OWN) << PIECE_SHIFT : fe;
+            put_ptrs<FUSED>(A.ptr, A.pbase, pend, fo, hown, sc, nf + depth, A.gen);
+        }
+        bool pending = mine && pf + WALK_PTR_OWN < pl;
+        while (__ballot(pending)) {
+            const u64 gm = (__ballot(pending) >> gb) & gmask;
+            const u32 li = gm ? (u32)__builtin_ctzll(gm) : 0u;
+            const u32 src = gb + li;
+            const u64 a = __shfl(fo, (int)src), b = __shfl(fe, (int)src);
+            const u32 kk = nf + (u32)__shfl((int)depth, (int)src);
+            if (gl == li) pending = false;
+            if (gm) put_ptrs<FUSED>(A.ptr, A.pbase, pend, a, b, sc, kk, A.gen, WALK_PTR_OWN + gl, WALK_G);
         }
         // the last consumed frame's lane: the stopping lane if it consumed, else the one before it
         const u32 llast = (code_m == 1 || code_m == 2 || mm == G) ? lm
@@ -305,16 +327,18 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             if (st_m == WEBSOCKET_SEG_ERR_LEN_WRAP) nonu = true;
         }
         active = false;
-        if (gl == 0) {
+        // the group's 16 lanes together: the pieces starting in the gap before the segment
+        // (fused; the classic walk wrote them first), in its tail, and past the batch's last one
+        {
             const u32 cnt = nf + extra;
             const u32 nofr = FUSED ? FUSED_NOFRAME : 0u;
-            if (FUSED) {                                                    // the gap before the segment
-                wait_stores();
-                put_ptrs<true>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, nofr, A.gen);
-            }
-            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt | nofr, A.gen);   // pieces starting in the tail
+            if (FUSED) put_ptrs<true>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, nofr, A.gen, gl, G);
+            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt | nofr, A.gen, gl, G);
             if (sc == A.nseg - 1)
-                put_ptrs<FUSED>(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, A.gen);
+                put_ptrs<FUSED>(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, A.gen, gl, G);
+        }
+        if (gl == 0) {
+            const u32 cnt = nf + extra;
             ws_store_res(A.res + sc, off, nf, status);
             if (!FUSED) {
                 *gptr<u32>(A.nwork + sc) = cnt;
@@ -380,7 +404,7 @@ struct FusedHead {
     u32 pad[8];
 };
 static_assert(sizeof(FusedHead) == 64, "fused head");
-#define FUSED_SPINS (1u << 16)    // polls (s_sleep 2 each) before a wave gives up waiting (tens of ms)
+#define FUSED_SPINS (1u << 17)    // polls (s_sleep 4 each, ~1 us with the load) before a wave gives up (~0.1 s)
 
 // Polls are vector loads with sc1 (L1 bypass; MI355X_MICROARCH.md: scalar loads go through the
 // scalar cache, which another CU's stores never refresh), one lane's word read by every lane.
@@ -396,7 +420,7 @@ __device__ __forceinline__ bool poll_done(const u64* done, u32 s, u32 gen, u32& 
             cnt = (u32)d;
             return true;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(4);
     }
     return false;
 }
@@ -458,7 +482,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
                 ok = !(vd & 1);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(4);
             w = poll8(lane < 5 ? paddr : pt + 2 * pidx);
         }
         // this piece: lanes 1-2 = {s, tag}, {k, tag}; the next one: lanes 3-4
@@ -615,7 +639,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
             go = false;
             for (u32 spins = 0; spins < FUSED_SPINS && !go; ++spins) {
                 go = (u32)poll8(reinterpret_cast<const u64*>(&A.head->donew)) == A.gen;
-                if (!go) __builtin_amdgcn_s_sleep(2);
+                if (!go) __builtin_amdgcn_s_sleep(4);
             }
         }
         if (go)
