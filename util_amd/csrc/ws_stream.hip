@@ -744,11 +744,14 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     const u64 send = len - P > RW_SAMPLE ? P + RW_SAMPLE : len;
     const SwOut o = stream_walk(buf, len, P, fresh ? 0 : sd->g, nf, send, false, max_frames, desc, items, ptr, pend,
                                 nwork, res, lane, plan->sample_out);
-    // the next call on this stream may skip the pass rounds while the sample's lengths keep
-    // changing (>= 8 frames, fewer than 4 per header round; a stream of runs or equal frames: rounds)
-    if (mirror && lane == 0)
-        __hip_atomic_store(&mirror->walk_hint, !o.ended && o.nf - nf >= 8 && (u64)o.steps * 4 > (u64)(o.nf - nf) ? 1u : 0u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the next call on this stream skips the pass rounds unless the sample looks like runs of
+    // equal lengths (>= 3 frames and >= 4 per header round, the round that met the sample's end
+    // not counted) or the stream ended in it
+    if (mirror && lane == 0) {
+        const u64 fr = o.nf - nf, st = o.steps > 1 ? o.steps - 1 : 1;
+        __hip_atomic_store(&mirror->walk_hint, !o.ended && !(fr >= 3 && fr >= 4 * st) ? 1u : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (o.ended) {
         if (lane == 0) plan->active = 0;
         return;
