@@ -208,10 +208,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
 
 /* Launch tuning knobs (for in-process A/B measurement; defaults are the tuned
  * configuration; every value yields bit-identical results, each one is parity-tested in
- * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_fused"
- * (path 3, eager calls: 0 the scan kernel then the unmask kernel, 1 both in one launch — walker
- * blocks ahead of the unmask blocks, hand-off through tagged words; captured calls always take
- * two launches), "fused_walkers" (walker blocks of the fused launch, 1..4096), "piece_lds"
+ * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "piece_lds"
  * (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
@@ -226,9 +223,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
 
-/* Counters (diagnostics): "fused_calls" (path-3 calls that took the fused launch, since load),
- * "fused_fails" (unmask waves of fused calls that gave up waiting for their walker blocks and
- * stored nothing — never expected; reading it synchronizes the devices), "workspace_bytes" (device bytes held
+/* Counters (diagnostics): "workspace_bytes" (device bytes held
  * in workspace slots), and of the calling process's most recent call: "stream_rw_chunks"
  * (chunks of a long stream written from the chunk-parallel walk's records),
  * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront), "stream_skips" (eager raw-stream

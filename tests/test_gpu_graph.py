@@ -298,47 +298,3 @@ def test_capture_only_process_reuses_dead_slots(dev, kind):
     for _ in range(30):
         cycle()
     assert W.get_stat("workspace_bytes") <= base, (base, W.get_stat("workspace_bytes"))
-
-
-def test_fused_option_eager_and_captured(dev):
-    """piece_fused 1: eager calls take the one-launch form, a captured call the two-launch one
-    (the fused form's tags are per call); alternating eager calls and replays on one batch stay
-    bit-exact, and no fused wave gave up waiting"""
-    name, wire, so, sl, mf = next(b for b in _batches() if b[0] == "random")
-    n = len(wire)
-    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
-    src = torch.from_numpy(wire).to(dev)
-    so_t = torch.tensor(so, dtype=torch.int64, device=dev)
-    sl_t = torch.tensor(sl, dtype=torch.int64, device=dev)
-    desc = torch.zeros(len(so) * mf * 32, dtype=torch.uint8, device=dev)
-    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
-    ob = wire.copy()
-    od, orr = oracle_segments(ob, so, sl, mf)
-    W.set_option("path", 3)
-    W.set_option("piece_fused", 1)
-    try:
-        f0 = W.get_stat("fused_calls")
-        d[:n].copy_(src)
-        W.batch_decode_device(d, so_t, sl_t, mf, desc, res)
-        torch.cuda.synchronize()
-        assert W.get_stat("fused_calls") == f0 + 1
-        assert np.array_equal(d[:n].cpu().numpy(), ob)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            W.batch_decode_device(d, so_t, sl_t, mf, desc, res)
-        assert W.get_stat("fused_calls") == f0 + 1                     # captured: two launches
-        for rnd in range(3):
-            d[:n].copy_(src)
-            res.zero_()
-            if rnd == 1:
-                W.batch_decode_device(d, so_t, sl_t, mf, desc, res)   # eager between replays
-            else:
-                g.replay()
-            torch.cuda.synchronize()
-            assert np.array_equal(d[:n].cpu().numpy(), ob), rnd
-            assert np.array_equal(res.cpu().numpy().view(W.SEGRES_DTYPE), orr), rnd
-        del g
-        assert W.get_stat("fused_fails") == 0
-    finally:
-        W.set_option("path", -1)
-        W.set_option("piece_fused", 0)

@@ -26,18 +26,12 @@ def dev():
 
 
 # decode variants: -1 auto (the default: 4 for many small segments, else 3), 3 the piece path
-# (scan kernel + one-shot 16 KiB piece unmask), 5 = path 3 as ONE launch (piece_fused: walker
-# blocks ahead of the unmask blocks), 4 one workgroup per segment (segfuse)
-@pytest.fixture(params=[(-1, 0), (3, 0), (3, 1), (4, 0)], ids=["auto", "piece", "fused", "segfuse"], autouse=True)
+# (scan kernel + one-shot 16 KiB piece unmask), 4 one workgroup per segment (segfuse)
+@pytest.fixture(params=[-1, 3, 4], ids=["auto", "piece", "segfuse"], autouse=True)
 def decode_path(request):
-    path, fused = request.param
-    W.set_option("path", path)
-    W.set_option("piece_fused", fused)
-    yield 5 if fused else path
+    W.set_option("path", request.param)
+    yield request.param
     W.set_option("path", -1)
-    W.set_option("piece_fused", 0)
-    if fused:
-        assert W.get_stat("fused_fails") == 0, "fused unmask waves gave up waiting"
 
 
 def gpu_decode(dev, host_buf, seg_off, seg_len, max_frames, desc_base=None, pad=64):
@@ -454,7 +448,7 @@ def test_stride_hint_never_changes_results(dev, decode_path):
     another frame length, or of the same first length with other lengths after it, or with
     bytes at the guessed stride that parse as frames of the guessed length: each decode is
     bit-exact vs the oracle whatever the hint was"""
-    if decode_path not in (3, 5):
+    if decode_path != 3:
         pytest.skip("the hint is the piece path's")
     primer = {}
     for plen in (4096, 1000, 125):

@@ -30,12 +30,6 @@ extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
-extern WsOpt ws_piece_fused, ws_fused_walkers;
-size_t ws_fused_bytes(u64 span, u32 nseg, u32 max_frames);
-int ws_launch_piece_fused(const WsLaunch& L, u64 lo, u64 hi, unsigned char* fb, u32 gen, int* advice, u32 g0,
-                          bool* fallback_needed);
-static int fused_fails(unsigned long long* out);
-extern std::atomic<unsigned long long> ws_stat_fused_calls;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
@@ -109,14 +103,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
     }
-    else if (!strcmp(name, "piece_fused")) {
-        if (value < 0 || value > 1) return -1;
-        ws_piece_fused = (int)value;
-    }
-    else if (!strcmp(name, "fused_walkers")) {
-        if (value < 1 || value > 4096) return -1;
-        ws_fused_walkers = (int)value;
-    }
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = value ? 1 : 0;
         ws_k2_timing_reset();
@@ -137,8 +123,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
     else if (!strcmp(name, "stream_skips")) *value = ws_stat_stream_skips.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
-    else if (!strcmp(name, "fused_calls")) *value = ws_stat_fused_calls.load();
-    else if (!strcmp(name, "fused_fails")) return fused_fails(value);
+
     else return -1;
     return 0;
 }
@@ -165,9 +150,6 @@ struct WsStreamWs {
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
-    void* fws = nullptr;           // fused decode buffer (ws_piece.hip): head + gen-tagged tables, zeroed at allocation
-    size_t fws_bytes = 0;
-    u32 fws_gen = 0;               // the last generation tag used in it (a wrapped tag re-zeroes it)
     void* aws = nullptr;           // auxiliary device scratch (the stream path's chunk-parallel walk)
     size_t aws_bytes = 0;
     void* hws = nullptr;           // ... and its pinned host copy
@@ -187,36 +169,11 @@ struct WsDevState {
 };
 static WsDevState g_dev[WS_MAX_DEV];
 static std::mutex g_dev_mu;        // device init and the stream-slot table
-std::atomic<unsigned long long> ws_stat_fused_calls{0};
-
-// unmask waves of fused calls that gave up waiting for their walker blocks (each such wave stores
-// nothing: never expected; tests assert 0): the heads' counters of every slot, read after a device
-// synchronize
-static int fused_fails(unsigned long long* out) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    unsigned long long t = 0;
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    for (int d = 0; d < WS_MAX_DEV; ++d)
-        for (auto& w : g_dev[d].sw) {
-            if (!w.fws) continue;
-            u32 head[16];
-            hipError_t e = hipSetDevice(d);
-            if (e == hipSuccess) e = hipDeviceSynchronize();
-            if (e == hipSuccess) e = hipMemcpy(head, w.fws, 64, hipMemcpyDeviceToHost);
-            if (e != hipSuccess) { (void)hipSetDevice(cur); return ws_set_err("fused_fails", e); }
-            t += head[7];
-        }
-    (void)hipSetDevice(cur);
-    *out = t;
-    return 0;
-}
-
 size_t ws_workspace_bytes_total() {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     size_t t = 0;
     for (auto& d : g_dev)
-        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes + w.fws_bytes;
+        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes;
     return t;
 }
 
@@ -256,16 +213,14 @@ static bool capturing(hipStream_t stream) {
 static void slot_free(WsStreamWs& w) {
     (void)hipFree(w.ws);
     (void)hipFree(w.ews);
-    (void)hipFree(w.fws);
     (void)hipFree(w.aws);
     if (w.hws) (void)hipHostFree(w.hws);
     if (w.adv_h) (void)hipHostFree(w.adv_h);
     for (void* p : w.retired) (void)hipFree(p);
     w.retired.clear();
-    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.fws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
+    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
     w.adv_h = nullptr; w.adv_d = nullptr;
-    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = w.fws_bytes = 0;
-    w.fws_gen = 0;
+    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = 0;
     w.aux_state_ok = false;
     w.stream = nullptr;
     w.capture = 0;
@@ -460,24 +415,6 @@ int WsSlot::workspace(size_t bytes, size_t zero_bytes, void** out) {
     return 0;
 }
 
-// the fused decode's buffer (eager calls only): zeroed whole at every (re)allocation, so every
-// tag in it is 0 or an earlier call's generation; when the generation counter wraps (2^32 calls)
-// it is zeroed again before the tag is reused
-int WsSlot::fused(size_t bytes, u32 gen, void** out) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    if (capturing(st)) return ws_set_msg("fused decode buffer: not for captured calls");
-    const size_t had = w->fws_bytes;
-    int rc = grow(w, &w->fws, &w->fws_bytes, bytes, st, (size_t)-1, "hipMalloc(fused decode buffer)");
-    if (rc) return rc;
-    if (w->fws_bytes == had && gen <= w->fws_gen) {
-        hipError_t e = hipMemsetAsync(w->fws, 0, w->fws_bytes, st);
-        if (e != hipSuccess) return ws_set_err("fused buffer re-zero", e);
-    }
-    w->fws_gen = gen;
-    *out = w->fws;
-    return 0;
-}
-
 int WsSlot::encode_workspace(size_t bytes, void** out) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     const int rc = grow(w, &w->ews, &w->ews_bytes, bytes, st, 0, "hipMalloc(encode workspace)");
@@ -594,18 +531,6 @@ int ws_decode_range(unsigned char* d_buf, u64 lo, u64 hi, const u64* d_seg_off, 
     // advised that nearly every segment held frames of one length (eager calls only)
     const u32 g0 = adv_h && __atomic_load_n(adv_h, __ATOMIC_RELAXED) == 1 ? (u32)__atomic_load_n(adv_h + 1, __ATOMIC_RELAXED)
                                                                          : 0u;
-    if (!ws && adv_h && ws_piece_fused && hi > lo) {
-        // one launch: walker blocks + unmask blocks (eager calls with the library's own workspace)
-        void* fb = nullptr;
-        if ((rc = slot.fused(ws_fused_bytes(hi - lo, nseg, max_frames), gen, &fb))) return rc;
-        bool nopieces = false;
-        rc = ws_launch_piece_fused(L, lo, hi, reinterpret_cast<unsigned char*>(fb), gen, adv_d, g0 >= 2 ? g0 : 0u,
-                                   &nopieces);
-        if (!nopieces) {
-            ++ws_stat_fused_calls;
-            return rc;
-        }
-    }
     if (!ws && need && (rc = slot.workspace(need, 16, &ws))) return rc;
     const u32* disorder = nullptr;
     bool fallback = false;

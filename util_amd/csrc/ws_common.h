@@ -415,7 +415,6 @@ struct WsSlot {
     int encode_workspace(size_t bytes, void** out);
     int aux(size_t dbytes, size_t hbytes, WsAux* out);
     int advice(int** host, int** dev);                             // the stride hint words (eager)
-    int fused(size_t bytes, u32 gen, void** out);                  // the fused decode's tagged tables (eager)
 };
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,

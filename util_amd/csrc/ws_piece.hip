@@ -37,68 +37,29 @@
 static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's chunks");
 #define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
 
-// ---- hand-off helpers of the fused form (ws_piece_fused_kernel below). Walker waves publish with
-// write-through (sc1) stores, wait for them (vmcnt(0)), then store a generation-tagged word; the
-// unmask waves poll tagged words and read the published items with sc1 vector loads (L1 bypass):
-// MI355X_MICROARCH.md, "Workgroup dispatch, XCD placement & inter-workgroup visibility", hand-off
-// form of row 1 (hipMalloc memory).
-// (compiler-emitted 8-B atomic accesses, global_load/store_dwordx2 sc1: inline-asm stores would
-// escape the compiler's hazard handling — a VALU write to a store's data registers right after the
-// store issued tore 16-B items on the GPU — and inline-asm loads its wait-count tracking)
-__device__ __forceinline__ void st16_sc1(gu32x4* p, u32x4 v) {
-    u64* q = reinterpret_cast<u64*>(reinterpret_cast<uintptr_t>(p));
-    __hip_atomic_store(q, (u64)v.x | ((u64)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (u64)v.z | ((u64)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32x4 ld16_sc1(const gu32x4* p) {
-    u64* q = reinterpret_cast<u64*>(reinterpret_cast<uintptr_t>(p));
-    const u64 a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const u64 b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u32x4 v;
-    v.x = (u32)a; v.y = (u32)(a >> 32); v.z = (u32)b; v.w = (u32)(b >> 32);
-    return v;
-}
-__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 // item: w0 = P0 | rkey[15:0] << 48, w1 = P1 | rkey[31:16] << 48 (origin-relative bytes < 2^48)
-template <bool FUSED>
 __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
     const u64 w0 = p0 | ((u64)(rk & 0xFFFFu) << 48), w1 = p1 | ((u64)(rk >> 16) << 48);
     u32x4 q;
     q.x = (u32)w0; q.y = (u32)(w0 >> 32); q.z = (u32)w1; q.w = (u32)(w1 >> 32);
-    if (FUSED) st16_sc1(it, q);
-    else *it = q;
+    *it = q;
 }
 
-// pieces whose first byte is in [lo, hi) (origin-relative) get segment s, item k; only pieces
-// of the batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the
-// batch unordered, and its pointers are clipped here). Classic table: one u64 s << 32 | k per
-// piece. Fused table: 16 B {s, tag, k, tag} per piece, stored write-through (each 8-B half
-// carries the call's tag, so a half read before the store lands is never taken as current); k's
-// bit 31 (FUSED_NOFRAME) marks a pointer that is not a frame's (gap before the segment, tail):
-// a frame pointer is stored only after the items up to its frame have landed.
-// (start, stride: the lanes of a group write one range together, lane j the pieces j, j + stride, ...)
+// pieces whose first byte is in [lo, hi) (origin-relative) get s << 32 | k; only pieces of the
+// batch's table [pbase, pend) exist (a segment outside [lo, hi) of the call marks the batch
+// unordered, and its pointers are clipped here). start, stride: the lanes of a group write one
+// range together, lane j the pieces j, j + stride, ...
 __device__ __forceinline__ u64 first_piece(u64 lo, u64 pbase) {
     const u64 p = (lo + (1ull << PIECE_SHIFT) - 1) >> PIECE_SHIFT;
     return p > pbase ? p : pbase;
 }
-template <bool FUSED>
-__device__ __forceinline__ void put_ptrs(void* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u32 tag,
-                                         u64 start = 0, u64 stride = 1) {
-    for (u64 p = first_piece(lo, pbase) + start; (p << PIECE_SHIFT) < hi && p < pend; p += stride) {
-        if (FUSED) {
-            u32x4 q;
-            q.x = s; q.y = tag; q.z = k; q.w = tag;
-            st16_sc1(gptr<u32x4>(reinterpret_cast<u32x4*>(ptr) + (p - pbase)), q);
-        } else {
-            *gptr<u64>(reinterpret_cast<u64*>(ptr) + (p - pbase)) = ((u64)s << 32) | k;
-        }
-    }
+__device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u64 start = 0,
+                                         u64 stride = 1) {
+    for (u64 p = first_piece(lo, pbase) + start; (p << PIECE_SHIFT) < hi && p < pend; p += stride)
+        *gptr<u64>(ptr + (p - pbase)) = ((u64)s << 32) | k;
 }
 
-#define FUSED_NOFRAME 0x80000000u
-
-// What one segment walk needs (K1, and the walker blocks of the fused kernel).
+// What one segment walk needs (K1).
 struct WalkArgs {
     const unsigned char* buf;
     const u64* seg_off;
@@ -108,10 +69,10 @@ struct WalkArgs {
     WebsocketFrameDesc_t* desc;
     WebsocketSegResult_t* res;
     u32x4* items;
-    void* ptr;            // classic u64 table or fused 16-B table
-    u32* nwork;           // classic only
-    WsSegRec* segr;       // classic only
-    u32* disorder;        // classic only (the fused kernel checks the order in a phase of its own)
+    u64* ptr;
+    u32* nwork;
+    WsSegRec* segr;
+    u32* disorder;
     u32 gen;
     u64 pbase, lo, hi;
     u32 g0;
@@ -127,7 +88,6 @@ struct WalkArgs {
 // one length (or it stopped on an error).
 #define WALK_G 16
 #define WALK_PTR_OWN 4    // piece pointers of its frame a lane writes alone
-template <bool FUSED>
 __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active, u32 lane, u32& cnt_out,
                                            bool& nonu_out) {
     constexpr u32 G = WALK_G;
@@ -137,13 +97,13 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
     const u64 pend = A.hi + lead0 ? ((A.hi + lead0 - 1) >> PIECE_SHIFT) + 1 : 0;   // end of the piece table
     const u64 so = A.seg_off[sc], sl = A.seg_len[sc];
     const u64 prev_end = sc ? A.seg_off[sc - 1] + A.seg_len[sc - 1] : 0;
-    if (!FUSED && active && gl == 0 && (prev_end > so || so < A.lo || so > A.hi || sl > A.hi - so))
+    if (active && gl == 0 && (prev_end > so || so < A.lo || so > A.hi || sl > A.hi - so))
         *gptr<u32>(A.disorder) = A.gen;
     const u64 dbase = A.desc_base ? A.desc_base[sc] : (u64)sc * A.max_frames;
     const u64 ibase = (u64)sc * A.max_frames;
     const u64 sorg = so + lead0;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(A.buf + so);
-    if (!FUSED && active) put_ptrs<false>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, 0, gl, G);
+    if (active) put_ptrs(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, 0, gl, G);
     // g0: the stride guess of the first step (the host's hint, 0 = none): lane k parses off + k*g0
     // at once; lane 0's frame is always the true first one, so a wrong guess costs nothing but
     // its loads (code 1 at lane 0 takes the true length)
@@ -255,11 +215,10 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
         if (mine) {                                                         // consumed frames, in parallel
-            put_item<FUSED>(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
+            put_item(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
                             rotl32(h.key, 8u * (u32)(p0 & 3)));
             if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + depth, so + pos, h);
         }
-        if (FUSED) wait_stores();                                           // items out before their pointers
         // the pieces whose first byte lies in a consumed frame point at it: a lane writes its frame's
         // first WALK_PTR_OWN pieces; a longer frame's rest the group's 16 lanes write together
         // (one lane alone would take milliseconds over a multi-GiB frame)
@@ -268,7 +227,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         const u64 pl = phi < pend ? phi : pend;
         if (mine) {
             const u64 hown = pf + WALK_PTR_OWN < pl ? (pf + WALK_PTR_OWN) << PIECE_SHIFT : fe;
-            put_ptrs<FUSED>(A.ptr, A.pbase, pend, fo, hown, sc, nf + depth, A.gen);
+            put_ptrs(A.ptr, A.pbase, pend, fo, hown, sc, nf + depth);
         }
         bool pending = mine && pf + WALK_PTR_OWN < pl;
         while (__ballot(pending)) {
@@ -278,7 +237,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             const u64 a = __shfl(fo, (int)src), b = __shfl(fe, (int)src);
             const u32 kk = nf + (u32)__shfl((int)depth, (int)src);
             if (gl == li) pending = false;
-            if (gm) put_ptrs<FUSED>(A.ptr, A.pbase, pend, a, b, sc, kk, A.gen, WALK_PTR_OWN + gl, WALK_G);
+            if (gm) put_ptrs(A.ptr, A.pbase, pend, a, b, sc, kk, WALK_PTR_OWN + gl, WALK_G);
         }
         // the last consumed frame's lane: the stopping lane if it consumed, else the one before it
         const u32 llast = (code_m == 1 || code_m == 2 || mm == G) ? lm
@@ -327,23 +286,18 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             if (st_m == WEBSOCKET_SEG_ERR_LEN_WRAP) nonu = true;
         }
         active = false;
-        // the group's 16 lanes together: the pieces starting in the gap before the segment
-        // (fused; the classic walk wrote them first), in its tail, and past the batch's last one
+        // the group's 16 lanes together: the pieces starting in its tail, and past the batch's last
+        // segment
         {
             const u32 cnt = nf + extra;
-            const u32 nofr = FUSED ? FUSED_NOFRAME : 0u;
-            if (FUSED) put_ptrs<true>(A.ptr, A.pbase, pend, sc ? prev_end + lead0 : 0, sorg, sc, nofr, A.gen, gl, G);
-            put_ptrs<FUSED>(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt | nofr, A.gen, gl, G);
-            if (sc == A.nseg - 1)
-                put_ptrs<FUSED>(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, A.gen, gl, G);
+            put_ptrs(A.ptr, A.pbase, pend, walked_end, sorg + sl, sc, cnt, gl, G);
+            if (sc == A.nseg - 1) put_ptrs(A.ptr, A.pbase, pend, sorg + sl, A.hi + lead0, 0xFFFFFFFFu, 0xFFFFFFFFu, gl, G);
         }
         if (gl == 0) {
             const u32 cnt = nf + extra;
             ws_store_res(A.res + sc, off, nf, status);
-            if (!FUSED) {
-                *gptr<u32>(A.nwork + sc) = cnt;
-                put_item<false>(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)), sorg, sorg + sl, cnt);   // WsSegRec
-            }
+            *gptr<u32>(A.nwork + sc) = cnt;
+            put_item(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)), sorg, sorg + sl, cnt);   // WsSegRec
             cnt_out = cnt;
             nonu_out = nonu;
         }
@@ -358,14 +312,14 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(WalkArgs A, u32*
     const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / WALK_G;
     u32 cnt = 0;
     bool nonu = false;
-    walk_group<false>(A, s, s < A.nseg, lane, cnt, nonu);
+    walk_group(A, s, s < A.nseg, lane, cnt, nonu);
     if (nonuni) {                                                           // one atomic per wave, if any
         const u64 b = __ballot(lane % WALK_G == 0 && s < A.nseg && nonu);
         if (lane == 0 && b) atomicAdd(nonuni, (u32)__popcll(b));
     }
 }
 
-// K2's inputs (the classic kernel and the unmask blocks of the fused one)
+// K2's inputs
 struct UnmaskArgs {
     unsigned char* buf;
     const u64* seg_off;
@@ -373,7 +327,7 @@ struct UnmaskArgs {
     u32 nseg, max_frames;
     const u32x4* items;
     const u32* nwork;
-    const void* ptr;              // classic u64 table or fused 16-B table
+    const u64* ptr;
     const u32* disorder;
     u32 gen;
     u64 pbase, c_lo, c_hi;
@@ -385,53 +339,13 @@ struct UnmaskArgs {
     u32* nonuni;
     int* advice;
     const WsSegRec* segr;
-    // fused kernel only
-    const u64* done;              // per segment: cnt | tag << 32, stored once the segment's items are out
-    struct FusedHead* head;
-    u32 nwb;                      // walker blocks in front of the unmask blocks
 };
-
-// The fused kernel's head (its buffer's first 64 B, zeroed at allocation): the counters rest at
-// zero between calls (the last arriver resets them); the words are generation-tagged.
-struct FusedHead {
-    u64 verdict;                  // gen << 1 | unordered: the order check's outcome
-    u32 cnt_check;                // walker blocks done with the order check
-    u32 cnt_done;                 // walker blocks done walking
-    u32 disw;                     // = gen: some walker block found the segments unordered
-    u32 nonuni;                   // segments whose frames are not all of one length
-    u32 donew;                    // = gen: every walker block is done
-    u32 fails;                    // unmask waves that gave up waiting (never expected)
-    u32 pad[8];
-};
-static_assert(sizeof(FusedHead) == 64, "fused head");
-#define FUSED_SPINS (1u << 17)    // polls (s_sleep 4 each, ~1 us with the load) before a wave gives up (~0.1 s)
-
-// Polls are vector loads with sc1 (L1 bypass; MI355X_MICROARCH.md: scalar loads go through the
-// scalar cache, which another CU's stores never refresh), one lane's word read by every lane.
-__device__ __forceinline__ u64 poll8(const u64* p) {
-    return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// poll segment s's tagged item count (wave-uniform): true when current, false when the wait gave up
-__device__ __forceinline__ bool poll_done(const u64* done, u32 s, u32 gen, u32& cnt) {
-    for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
-        const u64 d = poll8(done + s);
-        if ((u32)(d >> 32) == gen) {
-            cnt = (u32)d;
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(4);
-    }
-    return false;
-}
 
 // K2 body. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
 // exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
 // all measured slower): nontemporal loads and stores, chunks wholly inside
 // segments stored whole (byte coverage by the visited segments), 2^wshift windows.
-// FUSED: the piece pointer, the order verdict and each segment's item count come from walker
-// blocks of the same launch (tagged words, polled); the items are read write-through.
-template <int NT, int SR, bool FUSED>
+template <int NT, int SR>
 __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -446,14 +360,6 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(A.buf) & ~(uintptr_t)15);
     const u64 c_lo = A.c_lo, c_hi = A.c_hi;
     // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
-    // fused: the first poll (lane 0 the order verdict, lanes 1-2 this piece's pointer, 3-4 the
-    // next one's) goes out before the payload loads, so its answer does not queue behind them
-    const u64* const pt = reinterpret_cast<const u64*>(A.ptr);
-    const u64 pnext = pidx + 1 < A.npieces ? pidx + 1 : pidx;
-    const u64* const paddr = lane == 0 ? &A.head->verdict : (lane < 3 ? pt + 2 * pidx + (lane - 1)
-                                                                      : pt + 2 * pnext + (lane & 1 ? 0 : 1));
-    u64 pw0 = 0;
-    if (FUSED) pw0 = poll8(lane < 5 ? paddr : pt + 2 * pidx);
     u32x4 v[PIECE_U];
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) {
@@ -466,59 +372,23 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     const u32 nseg = A.nseg;
     u32 s = nseg, k = 0, step = 16;
     bool exact = false;                                                     // the first load holds them all
-    bool ok = false, failed = false;
-    if (FUSED) {
-        // the order verdict and this piece's pointer (the next piece's too, if already current:
-        // it bounds the first item load, as below)
-        const u32 gen = A.gen;
-        failed = true;
-        u64 w = pw0;
-        for (u32 spins = 0; spins < FUSED_SPINS; ++spins) {
-            const u64 vd = (u64)__builtin_amdgcn_readlane((int)(u32)w, 0) | ((u64)(u32)__builtin_amdgcn_readlane((int)(w >> 32), 0) << 32);
-            const u32 t1 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 1);
-            const u32 t2 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 2);
-            if ((u32)(vd >> 1) == gen && ((vd & 1) || (t1 == gen && t2 == gen))) {
-                failed = false;
-                ok = !(vd & 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-            w = poll8(lane < 5 ? paddr : pt + 2 * pidx);
-        }
-        // this piece: lanes 1-2 = {s, tag}, {k, tag}; the next one: lanes 3-4
-        const u32 ps = (u32)__builtin_amdgcn_readlane((int)(u32)w, 1), pk = (u32)__builtin_amdgcn_readlane((int)(u32)w, 2);
-        if (ok && pvalid && ps != 0xFFFFFFFFu) {
-            s = ps;
-            k = pk & ~FUSED_NOFRAME;
-            // both pointers frame pointers of one segment: the items [k, k'] have landed and are
-            // all this piece needs — no wait for the segment's count
-            const u32 ns = (u32)__builtin_amdgcn_readlane((int)(u32)w, 3), nk = (u32)__builtin_amdgcn_readlane((int)(u32)w, 4);
-            const u32 n1 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 3), n2 = (u32)__builtin_amdgcn_readlane((int)(w >> 32), 4);
-            if (pnext != pidx && n1 == gen && n2 == gen && ns == s && !(pk & FUSED_NOFRAME) && !(nk & FUSED_NOFRAME) &&
-                nk >= k && nk - k < 16u) {
-                step = nk - k + 1;
-                exact = true;
-            }
-        }
-    } else {
-        const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-            reinterpret_cast<uintptr_t>(reinterpret_cast<const u64*>(A.ptr) + pidx));
-        // the next piece's first item: when it is in the same segment, the items that touch this
-        // piece are exactly [k, k_next], so the first load takes only those (long segments would
-        // otherwise load 16 per wave however few they need)
-        const u64 pn = pidx + 1 < A.npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-                                                  reinterpret_cast<uintptr_t>(reinterpret_cast<const u64*>(A.ptr) + pidx + 1))
-                                            : PIECE_NONE;
-        ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(A.disorder)) != A.gen;
-        // no early return: an exit branch here would be hoisted above the payload loads
-        if (ok && pvalid && pv != PIECE_NONE) {
-            s = (u32)(pv >> 32);
-            k = (u32)pv;
-        }
-        if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
-            step = (u32)pn - k + 1;
-            exact = true;
-        }
+    const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+        reinterpret_cast<uintptr_t>(A.ptr + pidx));
+    // the next piece's first item: when it is in the same segment, the items that touch this
+    // piece are exactly [k, k_next], so the first load takes only those (long segments would
+    // otherwise load 16 per wave however few they need)
+    const u64 pn = pidx + 1 < A.npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+                                              reinterpret_cast<uintptr_t>(A.ptr + pidx + 1))
+                                        : PIECE_NONE;
+    const bool ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(A.disorder)) != A.gen;
+    // no early return: an exit branch here would be hoisted above the payload loads
+    if (ok && pvalid && pv != PIECE_NONE) {
+        s = (u32)(pv >> 32);
+        k = (u32)pv;
+    }
+    if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
+        step = (u32)pn - k + 1;
+        exact = true;
     }
     u32 cov[PIECE_U];
 #pragma unroll
@@ -545,17 +415,10 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
             cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
         } else {
             slo = A.seg_off[s] + lead0; shi = slo + A.seg_len[s];
-            if (!FUSED) cnt = A.nwork[s];
+            cnt = A.nwork[s];
         }
         if (!first && slo >= r1) break;                                     // the next segment starts past us
         first = false;
-        if (FUSED) {
-            if (exact) cnt = k + step;                                      // items [k, k + step) landed
-            else if (!poll_done(A.done, s, A.gen, cnt)) {
-                failed = true;
-                break;
-            }
-        }
         {
             // segment bytes relative to this wave's range, clamped to [-16, RW + 16]
             const long long sa = (long long)(slo - r0), sb = (long long)(shi - r0);
@@ -575,10 +438,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
             const u32 j = k + lane;
             const bool valid = j < cnt && lane < step;
             u32x4 q = {0, 0, 0, 0};
-            if (valid) {
-                if (FUSED) q = ld16_sc1(gptr<u32x4>(A.items + (u64)s * A.max_frames + j));
-                else q = A.items[(u64)s * A.max_frames + j];
-            }
+            if (valid) q = A.items[(u64)s * A.max_frames + j];
             const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
             const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
             const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
@@ -614,41 +474,26 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     }
     // ---- 3. store (v[] holds the unmasked bytes): full chunks one 16-B store, edge chunks
     //         exactly the covered bytes
-    if (!failed) {
 #pragma unroll
-        for (int u = 0; u < PIECE_U; ++u) {
-            const u64 c = wc0 + (u64)(u * 64 + lane);
-            if (!cov[u] || c < c_lo || c >= c_hi) continue;
-            const u32x4 w = v[u];
-            if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
-                st16<NT>(w, base + c);
-            } else {
-                ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
-            }
+    for (int u = 0; u < PIECE_U; ++u) {
+        const u64 c = wc0 + (u64)(u * 64 + lane);
+        if (!cov[u] || c < c_lo || c >= c_hi) continue;
+        const u32x4 w = v[u];
+        if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
+            st16<NT>(w, base + c);
+        } else {
+            ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
         }
-    } else if (lane == 0) {
-        atomicAdd(&A.head->fails, 1u);                                      // nothing stored: the stat shows it
     }
-    // the segments are out of buffer order (or outside [lo, hi)): nothing was stored above; the
-    // batch is decoded here instead, one wavefront per segment (ws_walk.h). Fused: once every
-    // walker block is done (their descriptors are then final, and these walks rewrite them).
-    if (!ok && !failed) {
-        const u32 nblk = gridDim.x - (FUSED ? A.nwb : 0u);
-        bool go = true;
-        if (FUSED) {
-            go = false;
-            for (u32 spins = 0; spins < FUSED_SPINS && !go; ++spins) {
-                go = (u32)poll8(reinterpret_cast<const u64*>(&A.head->donew)) == A.gen;
-                if (!go) __builtin_amdgcn_s_sleep(4);
-            }
-        }
-        if (go)
-            for (u32 s2 = bx * (PIECE_T / 64) + wv; s2 < nseg; s2 += nblk * (PIECE_T / 64))
-                walk_segment<4, NT>(A.buf, s2, A.seg_off, A.seg_len, A.max_frames, A.desc_base, A.desc, A.res, lane);
+    // K1 found the segments out of buffer order (or outside [lo, hi)): nothing was stored
+    // above; the batch is decoded here instead, one wavefront per segment (ws_walk.h)
+    if (!ok) {
+        for (u32 s2 = bx * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
+            walk_segment<4, NT>(A.buf, s2, A.seg_off, A.seg_len, A.max_frames, A.desc_base, A.desc, A.res, lane);
     }
     // the host's stride hint for the next call (ws_api.hip): valid while at most 1/32 of the
     // segments had frames of more than one length (K1 has finished: its count is final)
-    if (!FUSED && A.advice && bx == 0 && tid == 0) {
+    if (A.advice && bx == 0 && tid == 0) {
         const u32 n = *gptr<u32>(A.nonuni);
         *gptr<u32>(A.nonuni) = 0;
         __hip_atomic_store(A.advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -659,103 +504,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
 
 template <int NT, int SR>
 __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(UnmaskArgs A) {
-    unmask_piece<NT, SR, false>(A, blockIdx.x);
-}
-
-// Segment index of walker task t: the tasks alternate between the segments from the start of the
-// batch (A = [0, s1)) and those from the middle (B = [s1, nseg), s1 ~ where K2's second window
-// starts), the order in which the unmask blocks' two windows reach them; the rest in order.
-__device__ __forceinline__ u32 task_seg(u64 t, u32 s1, u32 nseg) {
-    const u32 na = s1, nb = nseg - s1, m = na < nb ? na : nb;
-    if (t < 2ull * m) return (t & 1) ? s1 + (u32)(t >> 1) : (u32)(t >> 1);
-    const u32 r = (u32)(t - 2ull * m);
-    return na > nb ? m + r : s1 + m + r;
-}
-
-// The fused decode: K1's walks and K2's unmask in ONE launch. Blocks [0, nwb) are walker blocks:
-// (1) each checks the order of its share of the segment table, the last one to finish publishes
-// the verdict; (2) 16-lane groups walk the segments (walk_group, write-through items and tagged
-// piece pointers, then per segment a tagged item count) in the order the unmask blocks reach
-// them; (3) the last walker block to finish writes the host's stride hint. Blocks [nwb, grid) are
-// K2's unmask blocks: each issues its payload loads first, then polls its piece's pointer and
-// segment counts (walkers run ahead: dispatched first, they never wait on anything).
-__global__ __launch_bounds__(PIECE_T, 6) void ws_piece_fused_kernel(WalkArgs W, UnmaskArgs A) {
-    if (blockIdx.x >= A.nwb) {
-        unmask_piece<1, 0, true>(A, blockIdx.x - A.nwb);
-        return;
-    }
-    const u32 tid = threadIdx.x, lane = tid & 63, b = blockIdx.x, nwb = A.nwb, nseg = A.nseg;
-    FusedHead* const H = A.head;
-    // (1) order check of segments [b * chunk, (b + 1) * chunk)
-    const u32 chunk = (nseg + nwb - 1) / nwb;
-    const u64 sb = (u64)b * chunk, se0 = sb + chunk, se = se0 < nseg ? se0 : nseg;
-    bool bad = false;
-    for (u64 s = sb + tid; s < se; s += PIECE_T) {
-        const u64 so = W.seg_off[s], sl = W.seg_len[s];
-        const u64 prev_end = s ? W.seg_off[s - 1] + W.seg_len[s - 1] : 0;
-        bad |= prev_end > so || so < W.lo || so > W.hi || sl > W.hi - so;
-    }
-    if (__ballot(bad) && lane == 0) __hip_atomic_store(&H->disw, A.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wait_stores();
-    __syncthreads();
-    if (tid == 0) {
-        const u32 old = __hip_atomic_fetch_add(&H->cnt_check, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == nwb - 1) {
-            __hip_atomic_store(&H->cnt_check, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u32 d = __hip_atomic_load(&H->disw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&H->verdict, ((u64)A.gen << 1) | (d == A.gen ? 1ull : 0ull), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    // (2) segment walks, 16 lanes each; a wave publishes its four segments' counts once its own
-    // stores have landed
-    // s1 ~ the first segment of the unmask blocks' second window: one interpolation step from the
-    // middle of the table (it orders the walks only; any value gives the same result)
-    u32 s1 = nseg;
-    if (A.wshift == 1) {
-        const u64 lead0 = reinterpret_cast<uintptr_t>(W.buf) & 15;
-        const u64 x1 = ((A.pbase + A.ppw) << PIECE_SHIFT) - lead0;
-        const u32 sg = nseg / 2;
-        const u64 first = W.seg_off[0], last = W.seg_off[nseg - 1] + W.seg_len[nseg - 1];
-        const long long avg = last > first && (last - first) / nseg > 0 ? (long long)((last - first) / nseg) : 1;
-        long long g = (long long)sg + ((long long)x1 - (long long)W.seg_off[sg]) / avg;
-        s1 = (u32)(g < 0 ? 0 : (g > (long long)nseg ? (long long)nseg : g));
-    }
-    const u64 NG = (u64)nwb * (PIECE_T / WALK_G);
-    const u64 gg = (u64)b * (PIECE_T / WALK_G) + tid / WALK_G;
-    u32 nonu_n = 0;
-    for (u64 t = gg;; t += NG) {
-        const bool act = t < nseg;
-        if (!__ballot(act)) break;
-        const u32 s = act ? task_seg(t, s1, nseg) : nseg - 1;
-        u32 cnt = 0;
-        bool nonu = false;
-        walk_group<true>(W, s, act, lane, cnt, nonu);
-        wait_stores();
-        if (act && lane % WALK_G == 0)
-            __hip_atomic_store(const_cast<u64*>(A.done) + s, ((u64)A.gen << 32) | cnt, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        nonu_n += (u32)__popcll(__ballot(act && lane % WALK_G == 0 && nonu));
-    }
-    // (3) the last walker block: stride hint, and the word the unordered fallback waits for
-    if (lane == 0 && nonu_n) __hip_atomic_fetch_add(&H->nonuni, nonu_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wait_stores();
-    __syncthreads();
-    if (tid == 0) {
-        const u32 old = __hip_atomic_fetch_add(&H->cnt_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == nwb - 1) {
-            __hip_atomic_store(&H->cnt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u32 n = __hip_atomic_exchange(&H->nonuni, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u64 vd = __hip_atomic_load(&H->verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (A.advice) {
-                __hip_atomic_store(A.advice, !(vd & 1) && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(A.advice + 1, (int)ws_first_frame_len(W.buf, W.seg_off, W.seg_len, nseg),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            __hip_atomic_store(&H->donew, A.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    unmask_piece<NT, SR>(A, blockIdx.x);
 }
 
 // ws layout: [disorder u32 | nonuni u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
@@ -875,7 +624,6 @@ static UnmaskArgs unmask_args(const WsLaunch& L, const PieceWs& P, u32 gen, int*
     A.items = P.items; A.nwork = P.nwork; A.ptr = P.ptr; A.disorder = P.disorder; A.gen = gen; A.pbase = P.pbase;
     A.c_lo = P.c_lo; A.c_hi = P.c_hi; A.desc_base = L.desc_base; A.desc = L.desc; A.res = L.res; A.wshift = wshift;
     A.ppw = ppw; A.npieces = P.npieces; A.nonuni = P.nonuni; A.advice = advice; A.segr = P.segr;
-    A.done = nullptr; A.head = nullptr; A.nwb = 0;
     return A;
 }
 
@@ -918,69 +666,4 @@ int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 ge
     *disorder_out = P.disorder;
     *fallback_needed = P.npieces == 0;
     return 0;
-}
-
-// ---- the fused form (one launch: walker blocks + unmask blocks, ws_piece_fused_kernel)
-// buffer: [FusedHead 64 B][ptr: npieces x 16 B][done: nseg x 8 B, 16-B aligned][items: nseg*max_frames x 16 B]
-// "piece_fused" (option): 0 K1 + K2 (two launches), 1 the fused launch for eager calls (captured calls
-// always take K1 + K2: the fused tags are per call, a graph would replay one tag); "fused_walkers":
-// walker blocks in front of the unmask blocks (each one: 16 segment walks at a time).
-WsOpt ws_piece_fused{0};
-WsOpt ws_fused_walkers{64};
-
-size_t ws_fused_bytes(u64 span, u32 nseg, u32 max_frames) {
-    const u64 npieces = (span + 15) / (1ull << PIECE_SHIFT) + 2;
-    return 64 + npieces * 16 + (((size_t)nseg * 8 + 15) & ~(size_t)15) + (size_t)nseg * max_frames * 16 + 16;
-}
-
-bool ws_fused_enabled() { return ws_piece_fused != 0; }
-
-int ws_launch_piece_fused(const WsLaunch& L, u64 lo, u64 hi, unsigned char* fb, u32 gen, int* advice, u32 g0,
-                          bool* fallback_needed) {
-    if (L.max_frames >= FUSED_NOFRAME) {                                 // k's flag bit must be free
-        *fallback_needed = true;
-        return ws_set_msg("fused decode: max_frames >= 2^31");
-    }
-    const u64 lead0 = reinterpret_cast<uintptr_t>(L.buf) & 15;
-    const u64 lo_org = lo + lead0, hi_org = hi + lead0;
-    PieceWs P;
-    P.npieces = piece_count(lo_org, hi_org);
-    *fallback_needed = P.npieces == 0;
-    if (!P.npieces) return ws_set_msg("fused decode: no pieces");
-    P.pbase = lo_org >> PIECE_SHIFT;
-    P.c_lo = lo_org >> 4;
-    P.c_hi = (hi_org + 15) >> 4;
-    P.disorder = nullptr;
-    P.nonuni = nullptr;
-    P.nwork = nullptr;
-    P.segr = nullptr;
-    P.ptr = reinterpret_cast<u64*>(fb + 64);
-    size_t b = 64 + P.npieces * 16;
-    const u64* done = reinterpret_cast<const u64*>(fb + b);
-    b += ((size_t)L.nseg * 8 + 15) & ~(size_t)15;
-    P.items = reinterpret_cast<u32x4*>(fb + b);
-    size_t tslot = 0;
-    int rc;
-    const int timing = ws_k2_timing;
-    if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    const u32 wshift = piece_wshift(P.npieces);
-    const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
-    const u64 grid = ppw << wshift;
-    const int nw_opt = ws_fused_walkers;
-    const u64 nw_max = ((u64)L.nseg + (PIECE_T / WALK_G) - 1) / (PIECE_T / WALK_G);   // >= one segment per group
-    const u32 nwb = (u32)((u64)(nw_opt < 1 ? 1 : nw_opt) < nw_max ? (u64)(nw_opt < 1 ? 1 : nw_opt) : nw_max);
-    if (grid + nwb > 0x7FFFFFFFull) return ws_set_msg("fused decode: batch too large for one launch");
-    WalkArgs W;
-    W.buf = L.buf; W.seg_off = L.seg_off; W.seg_len = L.seg_len; W.nseg = L.nseg; W.max_frames = L.max_frames;
-    W.desc_base = L.desc_base; W.desc = L.desc; W.res = L.res; W.items = P.items; W.ptr = P.ptr; W.nwork = nullptr;
-    W.segr = nullptr; W.disorder = nullptr; W.gen = gen; W.pbase = P.pbase; W.lo = lo; W.hi = hi;
-    W.g0 = g0 < (1u << 31) ? g0 : 0u;
-    UnmaskArgs A = unmask_args(L, P, gen, advice, wshift, ppw);
-    A.done = done;
-    A.head = reinterpret_cast<FusedHead*>(fb);
-    A.nwb = nwb;
-    hipLaunchKernelGGL(ws_piece_fused_kernel, dim3((u32)(grid + nwb)), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, W, A);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return ws_set_err("ws_piece_fused_kernel launch", e);
-    return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
 }
