@@ -76,6 +76,7 @@ struct WalkArgs {
     u32 gen;
     u64 pbase, lo, hi;
     u32 g0;
+    u32 alpha_ok;         // option "scan_alpha": alphabet speculation allowed
 };
 
 // G = 16 lanes per segment, header walk by STRIDE SPECULATION: lane k of the group parses the
@@ -260,7 +261,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
                 if (mm) add_len((u32)g);
                 add_len((u32)ret_m);
                 // a step that confirmed one frame of a new length: lengths keep changing
-                alpha = mm == 0 && nf > 0 && na >= 2;
+                alpha = mm == 0 && nf > 0 && na >= 2 && A.alpha_ok;
                 g = (u32)ret_m;
             } else {
                 // a chain of three or more equal lengths: back to stride speculation
@@ -524,6 +525,10 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     return b + (size_t)nseg * max_frames * 16 + 16;
 }
 
+// "scan_alpha": 1 (default) the walk switches to alphabet speculation once lengths keep changing,
+// 0 stride speculation only (round 3's walk)
+WsOpt ws_scan_alpha{1};
+
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip). Segments lie in
 // [lo, hi) of L.buf. count_nonuniform: K1 counts segments with frames of several lengths
 // for the K2 that follows (ws_launch_piece); other users pass false.
@@ -551,6 +556,7 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     W.desc_base = L.desc_base; W.desc = L.desc; W.res = L.res; W.items = P.items; W.ptr = P.ptr; W.nwork = P.nwork;
     W.segr = P.segr; W.disorder = P.disorder; W.gen = gen; W.pbase = P.pbase; W.lo = lo; W.hi = hi;
     W.g0 = g0 < (1u << 31) ? g0 : 0u;
+    W.alpha_ok = ws_scan_alpha ? 1u : 0u;
     hipLaunchKernelGGL(ws_piece_scan_kernel, dim3(blocks), dim3(PSCAN_T), 0, L.stream, W,
                        count_nonuniform ? P.nonuni : nullptr);
     hipError_t e = hipGetLastError();
