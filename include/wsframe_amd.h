@@ -210,8 +210,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * configuration; every value yields bit-identical results, each one is parity-tested in
  * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "scan_alpha"
  * (the piece path's segment walk: 1 switches to alphabet speculation over the lengths seen so far
- * once lengths keep changing, 0 stride speculation only), "piece_xg" (1: the unmask kernel's two
- * windows hand out pieces in groups of four consecutive ones per XCD), "piece_lds"
+ * once lengths keep changing, 0 stride speculation only), "piece_lds"
  * (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the

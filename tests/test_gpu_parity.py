@@ -325,7 +325,7 @@ def test_int_truncation_real_size(dev, decode_path, total):
     del gb, ob, host
 
 
-@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0), ("piece_xg", 1),
+@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0),
                                      ("piece_lds", 1), ("piece_lds", 56000)])
 def test_window_mappings(dev, decode_path, opt, val):
     """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
@@ -347,7 +347,6 @@ def test_window_mappings(dev, decode_path, opt, val):
         W.set_option("piece_win", 1)
         W.set_option("seg_win", 1)
         W.set_option("piece_lds", 0)
-        W.set_option("piece_xg", 0)
 
 
 def test_cfg4_shape_vs_oracle(dev, decode_path):

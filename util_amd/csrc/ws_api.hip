@@ -31,7 +31,6 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
-extern WsOpt ws_piece_xg;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
@@ -104,10 +103,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_rounds")) {
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
-    }
-    else if (!strcmp(name, "piece_xg")) {
-        if (value < 0 || value > 1) return -1;
-        ws_piece_xg = (int)value;
     }
     else if (!strcmp(name, "scan_alpha")) {
         if (value < 0 || value > 1) return -1;

@@ -336,7 +336,6 @@ struct UnmaskArgs {
     WebsocketFrameDesc_t* desc;
     WebsocketSegResult_t* res;
     u32 wshift;
-    u32 xg;               // option "piece_xg": two windows, four consecutive pieces per XCD (see below)
     u64 ppw, npieces;
     u32* nonuni;
     int* advice;
@@ -354,17 +353,8 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
-    u64 pw = (u64)(bx & ((1u << A.wshift) - 1u)) * A.ppw + (bx >> A.wshift);
-    bool pvalid = pw < A.npieces;
-    if (A.xg) {
-        // piece_xg (two windows): blocks are dealt round-robin over the 8 XCDs (observed; speed
-        // only), so window block i runs on XCD slot i % 4: the window's pieces go out in groups of
-        // 16 with each slot taking 4 consecutive ones — a segment's item and record lines are
-        // then fetched into one XCD's L2 instead of four (the grid is padded to 16 per window)
-        const u64 i = bx >> 1, t = i >> 4, u = i & 15, loc = 16 * t + 4 * (u & 3) + (u >> 2);
-        pw = (u64)(bx & 1u) * A.ppw + loc;
-        pvalid = loc < A.ppw && pw < A.npieces;
-    }
+    const u64 pw = (u64)(bx & ((1u << A.wshift) - 1u)) * A.ppw + (bx >> A.wshift);
+    const bool pvalid = pw < A.npieces;
     const u64 pidx = pvalid ? pw : A.npieces - 1;
     const u64 pc0 = (A.pbase + pidx) << (PIECE_SHIFT - 4);                   // first chunk of the piece
     const u64 wc0 = pc0 + (u64)wv * (64 * PIECE_U);                          // this wave's 4 KiB: 256 chunks
@@ -582,7 +572,6 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 // process on three boxes: profiles/r03_k2_occupancy.log; round 2's K2 was best at 5). On
 // gfx950 (160 KiB per CU) that is 27,136 B.
 WsOpt ws_piece_lds{0};
-WsOpt ws_piece_xg{0};    // "piece_xg": 1 = the two windows' pieces in groups of 4 per XCD slot (unmask_piece)
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
@@ -640,7 +629,7 @@ static UnmaskArgs unmask_args(const WsLaunch& L, const PieceWs& P, u32 gen, int*
     A.buf = L.buf; A.seg_off = L.seg_off; A.seg_len = L.seg_len; A.nseg = L.nseg; A.max_frames = L.max_frames;
     A.items = P.items; A.nwork = P.nwork; A.ptr = P.ptr; A.disorder = P.disorder; A.gen = gen; A.pbase = P.pbase;
     A.c_lo = P.c_lo; A.c_hi = P.c_hi; A.desc_base = L.desc_base; A.desc = L.desc; A.res = L.res; A.wshift = wshift;
-    A.ppw = ppw; A.npieces = P.npieces; A.nonuni = P.nonuni; A.advice = advice; A.segr = P.segr; A.xg = 0;
+    A.ppw = ppw; A.npieces = P.npieces; A.nonuni = P.nonuni; A.advice = advice; A.segr = P.segr;
     return A;
 }
 
@@ -661,10 +650,8 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
     const u32 wshift = piece_wshift(P.npieces);
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
-    const bool xg = ws_piece_xg && wshift == 1;
-    const u64 grid = xg ? ((ppw + 15) & ~15ull) << 1 : ppw << wshift;
+    const u64 grid = ppw << wshift;
     UnmaskArgs A = unmask_args(L, P, gen, advice, wshift, ppw);
-    A.xg = xg ? 1u : 0u;
     if (P.segr)
         hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, A);
     else
