@@ -320,46 +320,35 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(WalkArgs A, u32*
     }
 }
 
-// K2's inputs
-struct UnmaskArgs {
-    unsigned char* buf;
-    const u64* seg_off;
-    const u64* seg_len;
-    u32 nseg, max_frames;
-    const u32x4* items;
-    const u32* nwork;
-    const u64* ptr;
-    const u32* disorder;
-    u32 gen;
-    u64 pbase, c_lo, c_hi;
-    const u64* desc_base;
-    WebsocketFrameDesc_t* desc;
-    WebsocketSegResult_t* res;
-    u32 wshift;
-    u64 ppw, npieces;
-    u32* nonuni;
-    int* advice;
-    const WsSegRec* segr;
-};
-
-// K2 body. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
+// K2. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
 // exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
 // all measured slower): nontemporal loads and stores, chunks wholly inside
 // segments stored whole (byte coverage by the visited segments), 2^wshift windows.
 template <int NT, int SR>
-__device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
+__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
+                                                                  const u64* __restrict__ seg_off,
+                                                                  const u64* __restrict__ seg_len, u32 nseg,
+                                                                  u32 max_frames, const u32x4* __restrict__ items,
+                                                                  const u32* __restrict__ nwork,
+                                                                  const u64* __restrict__ ptr,
+                                                                  const u32* __restrict__ disorder, u32 gen, u64 pbase,
+                                                                  u64 c_lo, u64 c_hi, const u64* __restrict__ desc_base,
+                                                                  WebsocketFrameDesc_t* __restrict__ desc,
+                                                                  WebsocketSegResult_t* __restrict__ res,
+                                                                  u32 wshift, u64 ppw, u64 npieces, u32* nonuni,
+                                                                  int* advice, const WsSegRec* __restrict__ segr) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
-    const u64 pw = (u64)(bx & ((1u << A.wshift) - 1u)) * A.ppw + (bx >> A.wshift);
-    const bool pvalid = pw < A.npieces;
-    const u64 pidx = pvalid ? pw : A.npieces - 1;
-    const u64 pc0 = (A.pbase + pidx) << (PIECE_SHIFT - 4);                   // first chunk of the piece
+    const u32 bx = blockIdx.x;
+    const u64 pw = (u64)(bx & ((1u << wshift) - 1u)) * ppw + (bx >> wshift);
+    const bool pvalid = pw < npieces;
+    const u64 pidx = pvalid ? pw : npieces - 1;
+    const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
     const u64 wc0 = pc0 + (u64)wv * (64 * PIECE_U);                          // this wave's 4 KiB: 256 chunks
-    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(A.buf) & ~(uintptr_t)15);
-    const u64 c_lo = A.c_lo, c_hi = A.c_hi;
+    gu32x4* const base = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(buf) & ~(uintptr_t)15);
     // ---- 1. payload loads (unconditional, clamped to the batch's chunks [c_lo, c_hi))
     u32x4 v[PIECE_U];
 #pragma unroll
@@ -370,31 +359,26 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     // ---- 2. items that touch this wave's range [r0, r1) (origin-relative bytes)
     constexpr long long RW = 64 * PIECE_U * 16;                             // this wave's bytes
     const u64 r0 = wc0 << 4, r1 = r0 + RW;
-    const u32 nseg = A.nseg;
-    u32 s = nseg, k = 0, step = 16;
-    bool exact = false;                                                     // the first load holds them all
     const u64 pv = *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-        reinterpret_cast<uintptr_t>(A.ptr + pidx));
+        reinterpret_cast<uintptr_t>(ptr + pidx));
     // the next piece's first item: when it is in the same segment, the items that touch this
     // piece are exactly [k, k_next], so the first load takes only those (long segments would
     // otherwise load 16 per wave however few they need)
-    const u64 pn = pidx + 1 < A.npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
-                                              reinterpret_cast<uintptr_t>(A.ptr + pidx + 1))
-                                        : PIECE_NONE;
-    const bool ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(A.disorder)) != A.gen;
+    const u64 pn = pidx + 1 < npieces ? *reinterpret_cast<const __attribute__((address_space(4))) u64*>(
+                                            reinterpret_cast<uintptr_t>(ptr + pidx + 1))
+                                      : PIECE_NONE;
+    const u32 ok = *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(disorder)) != gen;
+    u32 cov[PIECE_U];
+#pragma unroll
+    for (int u = 0; u < PIECE_U; ++u) cov[u] = 0;
     // no early return: an exit branch here would be hoisted above the payload loads
-    if (ok && pvalid && pv != PIECE_NONE) {
-        s = (u32)(pv >> 32);
-        k = (u32)pv;
-    }
+    u32 s = ok && pvalid && pv != PIECE_NONE ? (u32)(pv >> 32) : nseg, k = (u32)pv, step = 16;
+    bool exact = false;                                                     // the first load holds them all
     if (s < nseg && pn != PIECE_NONE && (u32)(pn >> 32) == s && (u32)pn >= k && (u32)pn - k < 16u) {
         step = (u32)pn - k + 1;
         exact = true;
     }
-    u32 cov[PIECE_U];
-#pragma unroll
-    for (int u = 0; u < PIECE_U; ++u) cov[u] = 0;
-    const u64 lead0 = reinterpret_cast<uintptr_t>(A.buf) & 15;
+    const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const int xl = (int)lane * 16;                                          // lane's byte offset in a 1 KiB row
     // Chunks that hold payload bytes and lie wholly inside segments are stored whole
     // (bytes the decode does not change are written back unchanged: one 16-B store
@@ -410,13 +394,12 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
         u32 cnt;
         if (SR) {
             const u32x4 R = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(
-                reinterpret_cast<uintptr_t>(A.segr + s));
+                reinterpret_cast<uintptr_t>(segr + s));
             const u64 w0 = (u64)R.x | ((u64)R.y << 32), w1 = (u64)R.z | ((u64)R.w << 32);
             slo = w0 & 0xFFFFFFFFFFFFull; shi = w1 & 0xFFFFFFFFFFFFull;
             cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
         } else {
-            slo = A.seg_off[s] + lead0; shi = slo + A.seg_len[s];
-            cnt = A.nwork[s];
+            slo = seg_off[s] + lead0; shi = slo + seg_len[s]; cnt = nwork[s];
         }
         if (!first && slo >= r1) break;                                     // the next segment starts past us
         first = false;
@@ -439,7 +422,7 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
             const u32 j = k + lane;
             const bool valid = j < cnt && lane < step;
             u32x4 q = {0, 0, 0, 0};
-            if (valid) q = A.items[(u64)s * A.max_frames + j];
+            if (valid) q = items[(u64)s * max_frames + j];
             const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
             const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
             const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
@@ -448,13 +431,13 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
             const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
             // wave-relative item range, clamped to [-16, RW + 16] (32-bit from here on)
             const long long ra = (long long)(P0 - r0), rb = (long long)(P1 - r0);
-            const int Ai = (int)(ra < -16 ? -16 : (ra > RW + 16 ? RW + 16 : ra));
-            const int Bi = (int)(rb < -16 ? -16 : (rb > RW + 16 ? RW + 16 : rb));
+            const int A = (int)(ra < -16 ? -16 : (ra > RW + 16 ? RW + 16 : ra));
+            const int B = (int)(rb < -16 ? -16 : (rb > RW + 16 ? RW + 16 : rb));
             u64 hm = __ballot(valid && lane < nlim && P1 > r0 && P0 < P1);
             while (hm) {
                 const int i = __builtin_ctzll(hm);
                 hm &= hm - 1;
-                const int a = __builtin_amdgcn_readlane(Ai, i), b = __builtin_amdgcn_readlane(Bi, i);
+                const int a = __builtin_amdgcn_readlane(A, i), b = __builtin_amdgcn_readlane(B, i);
                 const u32 key = (u32)__builtin_amdgcn_readlane((int)rk, i);
 #pragma unroll
                 for (int u = 0; u < PIECE_U; ++u) {
@@ -489,23 +472,18 @@ __device__ __forceinline__ void unmask_piece(const UnmaskArgs& A, u32 bx) {
     // K1 found the segments out of buffer order (or outside [lo, hi)): nothing was stored
     // above; the batch is decoded here instead, one wavefront per segment (ws_walk.h)
     if (!ok) {
-        for (u32 s2 = bx * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
-            walk_segment<4, NT>(A.buf, s2, A.seg_off, A.seg_len, A.max_frames, A.desc_base, A.desc, A.res, lane);
+        for (u32 s2 = blockIdx.x * (PIECE_T / 64) + wv; s2 < nseg; s2 += gridDim.x * (PIECE_T / 64))
+            walk_segment<4, NT>(buf, s2, seg_off, seg_len, max_frames, desc_base, desc, res, lane);
     }
     // the host's stride hint for the next call (ws_api.hip): valid while at most 1/32 of the
     // segments had frames of more than one length (K1 has finished: its count is final)
-    if (A.advice && bx == 0 && tid == 0) {
-        const u32 n = *gptr<u32>(A.nonuni);
-        *gptr<u32>(A.nonuni) = 0;
-        __hip_atomic_store(A.advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(A.advice + 1, (int)ws_first_frame_len(A.buf, A.seg_off, A.seg_len, nseg), __ATOMIC_RELAXED,
+    if (advice && bx == 0 && tid == 0) {
+        const u32 n = *gptr<u32>(nonuni);
+        *gptr<u32>(nonuni) = 0;
+        __hip_atomic_store(advice, ok && (u64)n * 32 <= nseg ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(advice + 1, (int)ws_first_frame_len(buf, seg_off, seg_len, nseg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
-}
-
-template <int NT, int SR>
-__global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(UnmaskArgs A) {
-    unmask_piece<NT, SR>(A, blockIdx.x);
 }
 
 // ws layout: [disorder u32 | nonuni u32 | pad to 16][ptr: npieces u64][nwork: nseg u32][items: nseg*max_frames x 16 B]
@@ -624,15 +602,6 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
     return 0;
 }
 
-static UnmaskArgs unmask_args(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice, u32 wshift, u64 ppw) {
-    UnmaskArgs A;
-    A.buf = L.buf; A.seg_off = L.seg_off; A.seg_len = L.seg_len; A.nseg = L.nseg; A.max_frames = L.max_frames;
-    A.items = P.items; A.nwork = P.nwork; A.ptr = P.ptr; A.disorder = P.disorder; A.gen = gen; A.pbase = P.pbase;
-    A.c_lo = P.c_lo; A.c_hi = P.c_hi; A.desc_base = L.desc_base; A.desc = L.desc; A.res = L.res; A.wshift = wshift;
-    A.ppw = ppw; A.npieces = P.npieces; A.nonuni = P.nonuni; A.advice = advice; A.segr = P.segr;
-    return A;
-}
-
 static u32 piece_wshift(u64 npieces) {
     const int pwin = ws_piece_win;
     u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
@@ -651,11 +620,16 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const u32 wshift = piece_wshift(P.npieces);
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
-    UnmaskArgs A = unmask_args(L, P, gen, advice, wshift, ppw);
     if (P.segr)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, A);
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
+                           advice, (const WsSegRec*)P.segr);
     else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream, A);
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+                           L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
+                           advice, (const WsSegRec*)nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
     return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
