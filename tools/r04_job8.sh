@@ -1,6 +1,6 @@
-# round-4: same-box A/B of the round-3 library (ab_r03/, built from c51ee51) against this one
+# round-4: cfg4 K2 difference r03 vs r04 — which K1 change (cooperative pointers, early end)?
 set -o pipefail
-T=${1:-r04l}
+T=${1:-r04n}
 one() {  # tag, bench path, args
   timeout -k 10 300 python $2 $3 --no-cpu --no-e2e --no-xor-stream > gpurun_out/ab_one.json 2>/dev/null || { echo "FAIL $1"; exit 1; }
   python -c "
@@ -10,14 +10,6 @@ print('$1', '$3', d['ms_per_step'], r['frac'], r.get('kernel_ms_mean'), d['verif
 for r in 1 2; do
   one r03 ab_r03/bench.py "--config cfg4 --steps 4 --warmup 1"
   one r04 bench.py "--config cfg4 --steps 4 --warmup 1"
-done
-for r in 1 2; do
-  one r03 ab_r03/bench.py "--steps 100 --warmup 20"
-  one r04 bench.py "--steps 100 --warmup 20"
-  one r03 ab_r03/bench.py "--config cfg3 --steps 20 --warmup 5"
-  one r04 bench.py "--config cfg3 --steps 20 --warmup 5"
-done
-for r in 1 2; do
-  one r03 ab_r03/bench.py "--op stream --config cfg3 --steps 10 --warmup 3"
-  one r04 bench.py "--op stream --config cfg3 --steps 10 --warmup 3"
+  one own64 ab_own64/bench.py "--config cfg4 --steps 4 --warmup 1"
+  one noearly ab_noearly/bench.py "--config cfg4 --steps 4 --warmup 1"
 done
