@@ -88,12 +88,8 @@ struct WalkArgs {
 // return lane gl == 0 of the group holds its item count and whether its frames were not all of
 // one length (or it stopped on an error).
 #define WALK_G 16
-#ifndef WALK_PTR_OWN
 #define WALK_PTR_OWN 4    // piece pointers of its frame a lane writes alone
-#endif
-#ifndef WALK_EARLY_END
-#define WALK_EARLY_END 1  // (A/B builds: 0 = a walk reaching the segment's end takes one more round)
-#endif
+
 __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active, u32 lane, u32& cnt_out,
                                            bool& nonu_out) {
     constexpr u32 G = WALK_G;
@@ -258,7 +254,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             nf += G;
             off += G * g;
             add_len((u32)g);
-            if (off < sl || !WALK_EARLY_END) continue;
+            if (off < sl) continue;
         } else if (code_m == 1) {                                           // consumed, next length unknown
             nf += mm;
             if (!alpha) {
@@ -279,7 +275,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             }
             nf += 1;
             off = pos_m + (u32)ret_m;
-            if (off < sl || !WALK_EARLY_END) continue;
+            if (off < sl) continue;
         } else {
             nf += mm;
             off = pos_m;
