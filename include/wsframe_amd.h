@@ -220,8 +220,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream: chunk-parallel
  * walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront; log2 of its
  * largest chunk 16..26, pass rounds of a captured call 1..64, a captured
- * call's chunk records linked in parallel 0/1), "stream_own" (the chunk walk's owner walks: 1 by
- * 16-lane groups with stride/alphabet speculation, 0 one lane each), "k2_timing" (see
+ * call's chunk records linked in parallel 0/1), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);

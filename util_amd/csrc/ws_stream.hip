@@ -656,178 +656,6 @@ __global__ __launch_bounds__(RW_OWN_T) void ws_rw_own_kernel(const unsigned char
     own[oi] = ow;
 }
 
-// R3, group form ("stream_own" 1): 16 lanes per owner walk (four owners per wavefront), the
-// segment walk's speculation (ws_piece.hip walk_group): stride speculation over a run of equal
-// lengths, alphabet speculation (13 lanes over three frames) once lengths keep changing — the
-// owner's chain of dependent header loads shrinks ~2.4x on cfg3's mix. Outputs exactly the
-// serial form's (staging list, over, exit, count, end/dead), including the RW_MAXSTEPS cap.
-#define RW_OWN_G 16
-__global__ __launch_bounds__(64) void ws_rw_own16_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P, u64 C,
-                                                         u32 nchunks, u32 need_mask,
-                                                         const unsigned long long* __restrict__ dx,
-                                                         RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn,
-                                                         const RwPlan* __restrict__ plan) {
-    if (plan) {
-        if (!plan->active) return;
-        P = plan->P; C = plan->C; nchunks = plan->nchunks; need_mask = plan->need_mask; stgn = plan->stgn;
-    }
-    constexpr u32 G = RW_OWN_G;
-    const u32 lane = threadIdx.x, gl = lane % G, gb = lane - gl;
-    const u64 oi = (u64)blockIdx.x * (64 / G) + lane / G;
-    const bool exists = oi < (u64)nchunks * RW_D;
-    u64 pos = exists ? dx[oi] : 0;
-    bool active = exists && pos != 0;
-    const bool walked = active;
-    if (!__ballot(active)) return;
-    const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
-    const u64 c = exists ? oi / RW_D : 0, cs0 = P + c * C, cend = cs0 + C;
-    u32* const sl = stg + (exists ? oi : 0) * stgn;
-    u32 nb = 0, r = 0;
-    u64 over = 0, exitp = 0, g = 0;
-    bool alpha = false;
-    u32 L0 = 0, L1 = 0, L2 = 0, na = 0, rep = 0;
-    auto add_len = [&](u32 x) {                                              // (selects: no scratch array)
-        const bool add = x != 0 && x != L0 && !(na > 1 && x == L1) && !(na > 2 && x == L2);
-        const u32 at = na < 3 ? na : rep;
-        L0 = add && at == 0 ? x : L0;
-        L1 = add && at == 1 ? x : L1;
-        L2 = add && at == 2 ? x : L2;
-        rep = add && na == 3 ? (rep == 2 ? 0u : rep + 1) : rep;
-        na = add && na < 3 ? na + 1 : na;
-    };
-    auto len_at = [&](u32 i) -> u64 { return (u64)(i == 0 ? L0 : (i == 1 ? L1 : L2)); };
-    while (__ballot(active)) {
-        // this lane's candidate frame start and its depth in the chain
-        u64 pc = pos;
-        u32 d = 0;
-        bool cand = active;
-        if (!alpha) {
-            pc = pos + (u64)gl * g;
-            d = gl;
-            cand = active && (gl == 0 || g > 0);
-        } else if (gl >= 1) {
-            const u32 q = gl - 1;
-            if (q < na) { d = 1; pc = pos + len_at(q); }
-            else if (q - na < na * na) { const u32 t2 = q - na; d = 2; pc = pos + len_at(t2 / na) + len_at(t2 % na); }
-            else if (na == 2 && q - 6 < 8) {
-                const u32 t3 = q - 6;
-                d = 3;
-                pc = pos + len_at(t3 >> 2) + len_at((t3 >> 1) & 1) + len_at(t3 & 1);
-            } else cand = false;
-        }
-        // rw_step's rules: 3 past the chunk (stop before it), 1 the stream's walk ends there,
-        // 2 an implausible header (not the chain), 0 a frame of `ret` bytes
-        const bool ev = cand && pc < cend && pc < len && len - pc >= 2;
-        const uintptr_t pa = origin + (ev ? pc : 0);
-        const gu32x4* qh = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-        u64 h0, h1;
-        ws_hdr_from32(qh[0], qh[1], (u32)(pa & 15), h0, h1);
-        u32 code = 9, ret = 0;
-        if (cand) {
-            if (pc >= cend) code = 3;
-            else if (!ev) code = 1;
-            else if (!rw_plausible((u32)h0 & 0xFFu, (u32)(h0 >> 8) & 0xFFu, (u32)(h0 >> 16) & 0xFFFFu, need_mask)) code = 2;
-            else {
-                const WsHdr h = ws_parse(h0, h1, len - pc);
-                if (h.kind != WS_PARSE_FRAME || h.ret <= 0) code = 1;
-                else { code = 0; ret = (u32)h.ret; }
-            }
-        }
-        // the chain: depth t's lane; stride: the next lane while the length is g; alphabet: the
-        // child for the frame's length
-        u32 lc = 0, t = 0, qi = 0, cl1 = 0, cl2 = 0, cl3 = 0, stopc = 0;
-        for (;;) {
-            const u32 cc = (u32)__shfl((int)code, (int)(gb + lc));
-            if (cc != 0) { stopc = cc; break; }
-            const u32 rr = (u32)__shfl((int)ret, (int)(gb + lc));
-            if (!alpha) {
-                if (t + 1 < G && (u64)rr == g) { ++t; lc = t; continue; }
-                break;
-            }
-            const u32 idx = rr == L0 ? 0u : (na > 1 && rr == L1 ? 1u : (na > 2 && rr == L2 ? 2u : 3u));
-            const u32 maxd = na == 2 ? 3u : 2u;
-            if (idx == 3u || t == maxd) break;
-            qi = t == 0 ? idx : qi * na + idx;
-            lc = t == 0 ? 1 + qi : (t == 1 ? 1 + na + qi : 1 + na + na * na + qi);
-            if (t == 0) cl1 = lc; else if (t == 1) cl2 = lc; else cl3 = lc;
-            ++t;
-        }
-        const u32 ntake = stopc ? t : t + 1;                                // confirmed frames
-        auto lane_of = [&](u32 dd) -> u32 {
-            return alpha ? (dd == 0 ? 0u : (dd == 1 ? cl1 : (dd == 2 ? cl2 : cl3))) : dd;
-        };
-        const bool capped = active && (u64)nb + ntake > RW_MAXSTEPS;
-        const u32 keep = capped ? RW_MAXSTEPS + 1 - nb : ntake;
-        const bool mine = active && d < keep && gl == lane_of(d);
-        if (mine && nb + d < stgn) sl[nb + d] = (u32)(pc - cs0);            // the serial form's staging
-        {
-            const u64 om = (__ballot(mine && nb + d == stgn) >> gb) & 0xFFFFull;
-            const u64 ov = __shfl(pc, (int)(gb + (om ? __builtin_ctzll(om) : 0)));
-            if (om) over = ov;
-        }
-        // the last confirmed frame's end; the stopping lane's start
-        const u32 ll = lane_of(keep ? keep - 1 : 0);
-        const u64 lend = __shfl(pc, (int)(gb + ll)) + (u64)(u32)__shfl((int)ret, (int)(gb + ll));
-        const u64 ps = __shfl(pc, (int)(gb + lc));
-        // the chain's lengths (for the alphabet and the mode)
-        const u32 r0 = (u32)__shfl((int)ret, (int)gb), r1 = (u32)__shfl((int)ret, (int)(gb + lane_of(1)));
-        const u32 rl = (u32)__shfl((int)ret, (int)(gb + ll));
-        const u32 rx2 = (u32)__shfl((int)ret, (int)(gb + lane_of(2))), rx3 = (u32)__shfl((int)ret, (int)(gb + lane_of(3)));
-        if (!active) continue;
-        if (capped) {                                                        // RW_MAXSTEPS: dead
-            nb += keep;
-            exitp = lend;
-            r = 2;
-            active = false;
-            continue;
-        }
-        nb += ntake;
-        if (stopc) {
-            if (stopc == 3) {                                                // left the chunk
-                exitp = ps;
-                r = 0;
-            } else {                                                         // the walk ends (1) / dies (2) at ps
-                if (gl == 0 && nb < stgn) sl[nb] = (u32)(ps - cs0);
-                if (nb == stgn) over = ps;
-                exitp = ps;
-                r = stopc;
-            }
-            active = false;
-            continue;
-        }
-        pos = lend;
-        if (alpha) {
-            add_len(r0);
-            if (ntake > 1) add_len(r1);
-            if (ntake > 2) add_len(rx2);
-            if (ntake > 3) add_len(rx3);
-            if (ntake >= 3 && r0 == r1 && r0 == rl) {                        // three equal lengths: stride again
-                alpha = false;
-                g = rl;
-            }
-        } else {
-            if (ntake > 1) add_len((u32)g);                                  // (a stride chain: g, then its last)
-            add_len(rl);
-            if (ntake == 1 && g != 0 && (u64)r0 != g && na >= 2) alpha = true;
-            g = rl;
-        }
-        if (pos >= cend) {
-            exitp = pos;
-            r = 0;
-            active = false;
-        }
-    }
-    if (walked && gl == 0) {
-        RwOwn ow;
-        ow.exit = exitp;
-        ow.cs = nb | ((r == 1 ? 1u : 0u) << 31);
-        ow.dead = r == 2 ? 1u : 0u;
-        ow.over = over;
-        ow.pad = 0;
-        own[oi] = ow;
-    }
-}
-
 // emit: one wavefront per chain chunk, tab[b] = {entry, exit_w, nf0, cnt_w, owner, n_par,
 // last, cs0}: the window prefix [entry, exit_w) by the group walk, then n_par staged
 // frames in parallel (lane i: frame i, i + 64, ...), then the group walk from the next
@@ -1268,7 +1096,6 @@ WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long str
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
-WsOpt ws_stream_own{1};         // "stream_own": R3 owner walks by 16-lane groups with speculation (0: one lane each)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
@@ -1383,11 +1210,7 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
                        need_mask, cand, capc, recs, nrec, dx, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
-    if (ws_stream_own)
-        hipLaunchKernelGGL(ws_rw_own16_kernel, dim3((u32)((nchunks * RW_D + 3) / 4)), dim3(64), 0, st, d_buf, len, P,
-                       C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr);
-    else
-        hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len, P,
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len, P,
                        C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -1518,11 +1341,7 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
                        cand, nrec, 0u, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
-    if (ws_stream_own)
-        hipLaunchKernelGGL(ws_rw_own16_kernel, dim3((u32)((L.nch_cap * RW_D + 3) / 4)), dim3(64), 0, st, d_buf, len,
-                       (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
-    else
-        hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len,
+    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len,
                        (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
     if (ws_stream_plink) {          // the chunk-parallel linker; the serial one below exits if it linked
         RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
