@@ -38,38 +38,11 @@ static_assert((1 << PIECE_SHIFT) == PIECE_T * PIECE_U * 16, "piece = one block's
 #define PIECE_NONE 0xFFFFFFFFFFFFFFFFull
 
 // item: w0 = P0 | rkey[15:0] << 48, w1 = P1 | rkey[31:16] << 48 (origin-relative bytes < 2^48)
-// K1's stores (WALK_WT, A/B builds: write-through sc1 8-B stores, so no K1 line is left dirty in
-// an L2 at the K1 -> K2 boundary)
-#ifndef WALK_WT
-#define WALK_WT 0
-#endif
-__device__ __forceinline__ void k1_st8(void* p, u64 v) {
-    if (WALK_WT) __hip_atomic_store(reinterpret_cast<u64*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *gptr<u64>(p) = v;
-}
-__device__ __forceinline__ void k1_st16(void* p, u32x4 v) {
-    if (WALK_WT) {
-        k1_st8(p, (u64)v.x | ((u64)v.y << 32));
-        k1_st8(reinterpret_cast<u64*>(p) + 1, (u64)v.z | ((u64)v.w << 32));
-    } else {
-        *gptr<u32x4>(p) = v;
-    }
-}
 __device__ __forceinline__ void put_item(gu32x4* it, u64 p0, u64 p1, u32 rk) {
     const u64 w0 = p0 | ((u64)(rk & 0xFFFFu) << 48), w1 = p1 | ((u64)(rk >> 16) << 48);
     u32x4 q;
     q.x = (u32)w0; q.y = (u32)(w0 >> 32); q.z = (u32)w1; q.w = (u32)(w1 >> 32);
-    k1_st16(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(it)), q);
-}
-// the descriptor / segment result of ws_common.h, through K1's stores
-__device__ __forceinline__ void k1_store_desc(WebsocketFrameDesc_t* d, u64 frame_off, const WsHdr& h) {
-    const u64 dof = h.plen ? frame_off + h.hdr : WEBSOCKET_DATA_OFF_NULL;
-    u32x4 q0, q1;
-    q0.x = (u32)frame_off; q0.y = (u32)(frame_off >> 32); q0.z = (u32)dof; q0.w = (u32)(dof >> 32);
-    q1.x = (u32)h.plen; q1.y = (u32)(h.plen >> 32); q1.z = (u32)h.ret;
-    q1.w = (h.b0 >> 7) | ((h.b0 & 0x0Fu) << 8) | (h.masked << 16) | (h.hdr << 24);
-    k1_st16(d, q0);
-    k1_st16(reinterpret_cast<unsigned char*>(d) + 16, q1);
+    *it = q;
 }
 
 // pieces whose first byte is in [lo, hi) (origin-relative) get s << 32 | k; only pieces of the
@@ -83,7 +56,7 @@ __device__ __forceinline__ u64 first_piece(u64 lo, u64 pbase) {
 __device__ __forceinline__ void put_ptrs(u64* ptr, u64 pbase, u64 pend, u64 lo, u64 hi, u32 s, u32 k, u64 start = 0,
                                          u64 stride = 1) {
     for (u64 p = first_piece(lo, pbase) + start; (p << PIECE_SHIFT) < hi && p < pend; p += stride)
-        k1_st8(ptr + (p - pbase), ((u64)s << 32) | k);
+        *gptr<u64>(ptr + (p - pbase)) = ((u64)s << 32) | k;
 }
 
 // What one segment walk needs (K1).
@@ -246,7 +219,7 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         if (mine) {                                                         // consumed frames, in parallel
             put_item(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
                             rotl32(h.key, 8u * (u32)(p0 & 3)));
-            if (h.ret != 0) k1_store_desc(A.desc + dbase + nf + depth, so + pos, h);
+            if (h.ret != 0) ws_store_desc(A.desc + dbase + nf + depth, so + pos, h);
         }
         // the pieces whose first byte lies in a consumed frame point at it: a lane writes its frame's
         // first WALK_PTR_OWN pieces; a longer frame's rest the group's 16 lanes write together
@@ -324,13 +297,8 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         }
         if (gl == 0) {
             const u32 cnt = nf + extra;
-            {
-                u32x4 rq;
-                rq.x = (u32)off; rq.y = (u32)(off >> 32); rq.z = nf; rq.w = (u32)status;
-                k1_st16(A.res + sc, rq);                                    // ws_store_res
-            }
-            if (WALK_WT) __hip_atomic_store(A.nwork + sc, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else *gptr<u32>(A.nwork + sc) = cnt;
+            ws_store_res(A.res + sc, off, nf, status);
+            *gptr<u32>(A.nwork + sc) = cnt;
             put_item(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)), sorg, sorg + sl, cnt);   // WsSegRec
             cnt_out = cnt;
             nonu_out = nonu;
