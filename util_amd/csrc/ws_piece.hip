@@ -88,7 +88,7 @@ struct WalkArgs {
 // return lane gl == 0 of the group holds its item count and whether its frames were not all of
 // one length (or it stopped on an error).
 #define WALK_G 16
-#define WALK_PTR_OWN 4    // piece pointers of its frame a lane writes alone
+#define WALK_PTR_OWN 64   // piece pointers of its frame a lane writes alone (the rest: the group; with 4, cfg4 ran 7 % slower: profiles/r04_ptr_own_ab.log)
 
 __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active, u32 lane, u32& cnt_out,
                                            bool& nonu_out) {
