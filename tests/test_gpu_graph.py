@@ -163,6 +163,43 @@ def test_stream_decode_graph_replay(dev, case, plink):
         assert np.array_equal(d[:n].cpu().numpy(), ob), rnd
 
 
+def test_stream_graph_replays_follow_the_walk_hint(dev):
+    """a captured stream decode whose previous replay's chunk walk saw lengths that keep changing
+    skips its pass rounds on the device (they exit at once, the plan kernel starts the walk at 0);
+    a uniform stream then seen by that walk sends the replay after it back to the rounds. The
+    bytes change between replays (same length): every replay bit-exact vs the oracle"""
+    mixed, *_ = wsynth.make_batch(1500, wsynth.PLEN_MIX3, 0, 0, 48)
+    n = len(mixed)
+    uni, *_ = wsynth.make_batch(n // 4110 + 2, 0, 4096, 0, 5)
+    runs = np.concatenate([wsynth.make_batch(k, 0, fl, 0, 60 + i)[0]
+                           for i, (k, fl) in enumerate([(4000, 125), (3000, 1500), (n // 65550 + 2, 65536)])])
+    mixed2, *_ = wsynth.make_batch(1600, wsynth.PLEN_MIX3, 0, 0, 49)
+    assert len(uni) >= n and len(runs) >= n and len(mixed2) >= n
+    mf = 1 << 15
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(mf * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(16, dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        W.stream_decode_device(d, n, mf, desc, res)
+    # mixed (rounds, then the walk: hint set), mixed (skip), uniform (skip; hint cleared),
+    # uniform (rounds), runs, mixed2 cut mid-frame, mixed2 again, mixed
+    for rnd, w in enumerate([mixed, mixed, uni[:n], uni[:n], runs[:n], mixed2[:n], mixed2[:n], mixed]):
+        w = np.ascontiguousarray(w)
+        d[:n].copy_(torch.from_numpy(w).to(dev))
+        desc.zero_()
+        res.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        ob = w.copy()
+        od, orr = oracle_segments(ob, [0], [n], mf)
+        gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+        assert tuple(gr) == tuple(orr[0]), (rnd, gr, orr[0])
+        gd = desc.cpu().numpy().view(W.DESC_DTYPE)[:int(gr["n_frames"])]
+        assert np.array_equal(gd, od[:int(orr[0]["n_frames"])]), rnd
+        assert np.array_equal(d[:n].cpu().numpy(), ob), rnd
+
+
 FIRST_CALL = r"""
 import sys, numpy as np, torch
 sys.path[:0] = [sys.argv[1], sys.argv[2]]

@@ -87,6 +87,7 @@ struct SdState {
     u32 ticket;                      // resolve blocks done (the last one writes the state)
     u32 nf, extra, short_passes, phase;
     int status;
+    u32 walk_hint;                   // captured calls: the last chunk walk's hint (next replay: no rounds)
 };
 static_assert(sizeof(SdState) <= 128, "stream state");
 struct SdMirror {                    // pinned host copy of the state after a resolve (eager calls)
@@ -130,7 +131,9 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned 
                                                                  WebsocketFrameDesc_t* __restrict__ desc,
                                                                  u32x4* __restrict__ items, u64* __restrict__ ptr,
                                                                  u64 pend, SdState* __restrict__ sd,
-                                                                 u64* __restrict__ seg, u32* __restrict__ disorder) {
+                                                                 u64* __restrict__ seg, u32* __restrict__ disorder,
+                                                                 int dev_hint) {
+    if (dev_hint && sd->walk_hint) return;                                   // the chunk walk starts at 0
     if (first && part == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         seg[0] = 0;
         seg[1] = len;
@@ -272,9 +275,11 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_resolve_kernel(const unsign
                                                                     u64 pend, SdState* __restrict__ sd,
                                                                     u32* __restrict__ nwork,
                                                                     WebsocketSegResult_t* __restrict__ res,
-                                                                    SdMirror* __restrict__ mirror, u32 gen) {
+                                                                    SdMirror* __restrict__ mirror, u32 gen,
+                                                                    int dev_hint) {
     __shared__ u64 f_lo[2], f_hi[2], f_val[2];
     __shared__ int s_last;
+    if (dev_hint && sd->walk_hint) return;
     if (!first && sd->phase != SD_PASSES) {                                  // nothing left to resolve
         if (finish && blockIdx.x == 0 && threadIdx.x < 64 && sd->phase != SD_DONE)
             stream_walk(buf, len, sd->P, sd->g, sd->nf, len, true, max_frames, desc, items, ptr, pend, nwork, res,
@@ -717,7 +722,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
 #define RW_CAP_STGN 1024u      // ... and staging per owner
 
 __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __restrict__ buf, u64 len, u32 max_frames,
-                                                        const SdState* __restrict__ sd, RwPlan* __restrict__ plan,
+                                                        SdState* __restrict__ sd, RwPlan* __restrict__ plan,
                                                         u64 cmin, u64 cmax, u32 nchunks_cap, u64 cand_cap, u64 stg_cap,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
@@ -725,6 +730,9 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
                                                         SdMirror* __restrict__ mirror) {
     const u32 lane = threadIdx.x;
+    // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
+    const int dev = fresh == 2;
+    if (dev) fresh = sd->walk_hint != 0;
     if (!fresh && sd->phase == SD_DONE) {                                    // the passes finished it
         if (lane == 0) plan->active = 0;
         return;
@@ -747,10 +755,11 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     // the next call on this stream skips the pass rounds unless the sample looks like runs of
     // equal lengths (>= 3 frames and >= 4 per header round, the round that met the sample's end
     // not counted) or the stream ended in it
-    if (mirror && lane == 0) {
+    if (lane == 0) {
         const u64 fr = o.nf - nf, st = o.steps > 1 ? o.steps - 1 : 1;
-        __hip_atomic_store(&mirror->walk_hint, !o.ended && !(fr >= 3 && fr >= 4 * st) ? 1u : 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        const u32 hint = !o.ended && !(fr >= 3 && fr >= 4 * st) ? 1u : 0u;
+        if (mirror) __hip_atomic_store(&mirror->walk_hint, hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (dev) sd->walk_hint = hint;                                       // read by the next replay
     }
     if (o.ended) {
         if (lane == 0) plan->active = 0;
@@ -1318,7 +1327,7 @@ static RwDevLayout rw_dev_layout(u64 len) {
 }
 
 static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, WebsocketFrameDesc_t* d_desc,
-                          const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st, const SdState* sd,
+                          const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st, SdState* sd,
                           unsigned char* w, const RwDevLayout& L, int fresh = 0, u64* d_seg = nullptr,
                           SdMirror* mirror = nullptr) {
     RwPlan* plan = reinterpret_cast<RwPlan*>(w + L.o_plan);
@@ -1429,30 +1438,33 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     u64 kmax = std::min<u64>(std::min<u64>(len / 2 + 1, (u64)max_frames + 1), SD_KMAX);
     const u32 b_blocks = (u32)std::max<u64>(1, std::min<u64>((kmax + SPASS_T - 1) / SPASS_T, 8192));
     int round = 0;
-    auto rounds = [&](int n, bool finish_last, u32 tag) -> int {
+    auto rounds = [&](int n, bool finish_last, u32 tag, int dev_hint) -> int {
         for (int r = 0; r < n; ++r, ++round) {
             const int first = round == 0, fin = finish_last && r == n - 1;
             hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(SD_PROBE_K / SPASS_T), dim3(SPASS_T), 0, st, d_buf, (u64)len,
-                               max_frames, 0, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder);
+                               max_frames, 0, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder,
+                               dev_hint);
             hipLaunchKernelGGL(ws_stream_pass_kernel, dim3(b_blocks), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
-                               1, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder);
+                               1, first, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, d_seg, Pw.disorder, dev_hint);
             hipLaunchKernelGGL(ws_stream_resolve_kernel, dim3(64), dim3(SPASS_T), 0, st, d_buf, (u64)len, max_frames,
-                               first, fin, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, Pw.nwork, d_res, dm, tag);
+                               first, fin, d_desc, Pw.items, Pw.ptr, Pw.npieces, sd, Pw.nwork, d_res, dm, tag, dev_hint);
         }
         const hipError_t e2 = hipGetLastError();
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
     const int nr0 = ws_stream_rounds, nr = nr0 >= 1 && nr0 <= 64 ? nr0 : 4;
     if (dev_rw) {
-        if ((rc = rounds(nr, false, 0))) return rc;
+        // a replay whose previous replay's chunk walk saw lengths that keep changing skips the
+        // rounds on the device (they exit at once) and the plan kernel starts the walk at 0
+        if ((rc = rounds(nr, false, 0, 1))) return rc;
         if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
-                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL)))
+                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 2, d_seg)))
             return rc;
         *A.state_ok = true;
         return ws_launch_piece_unmask(L, Pw, gen);
     }
     if (!host_rw) {
-        if ((rc = rounds(nr, true, 0))) return rc;
+        if ((rc = rounds(nr, true, 0, 0))) return rc;
         *A.state_ok = true;
         return ws_launch_piece_unmask(L, Pw, gen);
     }
@@ -1483,10 +1495,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         return ws_launch_piece_unmask(L, Pw, gen);
     }
     u32 tag = ws_next_gen();
-    if ((rc = rounds(1, false, tag)) || (rc = published(tag))) return rc;
+    if ((rc = rounds(1, false, tag, 0)) || (rc = published(tag))) return rc;
     while (hm->phase == SD_PASSES) {
         tag = ws_next_gen();
-        if ((rc = rounds(1, false, tag)) || (rc = published(tag))) return rc;
+        if ((rc = rounds(1, false, tag, 0)) || (rc = published(tag))) return rc;
     }
     *A.state_ok = true;
     if (hm->phase != SD_DONE) {
