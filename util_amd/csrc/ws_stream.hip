@@ -158,19 +158,20 @@ struct SwOut {            // where a stream_walk stopped: the next frame, its in
     u64 next;
     u32 nf, ended;
     u32 steps;            // header rounds the walk took (a run of equal frames takes one per 64)
+    u32 maxlen;           // the longest frame it took (wire bytes; only when asked: want_max)
 };
 __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ buf, u64 len, u64 P0, u64 g0, u32 nf0,
                                             u64 end, bool last, u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
                                             u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                             u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
-                                            u32 lane, u64* __restrict__ out = nullptr) {
+                                            u32 lane, u64* __restrict__ out = nullptr, bool want_max = false) {
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const uintptr_t seg = reinterpret_cast<uintptr_t>(buf);
     u64 off = P0, g = g0, walked_end = lead0 + P0;
     u32 nf = nf0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
     bool at_bnd = false;
-    u32 steps = 0;
+    u32 steps = 0, mx = 0;
     for (;;) {
         ++steps;
         const u64 pos = off + (u64)lane * g;
@@ -209,6 +210,7 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
             if (h.ret != 0) ws_store_desc(desc + nf + lane, pos, h);
         }
         if (ntake) walked_end = __shfl(fe, (int)ntake - 1);
+        if (want_max && lane < ntake && h.ret > 0 && (u32)h.ret > mx) mx = (u32)h.ret;
         if (mm == 64) { nf += 64; off += 64 * g; continue; }
         const u64 pos_m = off + (u64)mm * g;
         const int ret_m = __builtin_amdgcn_readlane(h.ret, (int)mm);
@@ -235,6 +237,15 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
     r.nf = nf;
     r.ended = at_bnd ? 0u : 1u;
     r.steps = steps;
+    r.maxlen = 0;
+    if (want_max) {
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const u32 o2 = (u32)__shfl_xor((int)mx, d);
+            mx = o2 > mx ? o2 : mx;
+        }
+        r.maxlen = mx;
+    }
     if (!last && (at_bnd || !out)) return r;
     const u32 cnt = nf + extra;
     for (u64 p = ((walked_end + (1ull << PIECE_SHIFT_S) - 1) >> PIECE_SHIFT_S) + lane;
@@ -445,6 +456,18 @@ __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
     return v;
 }
 
+// The window at each chunk's start must hold a frame start of the chain: any window longer
+// than every frame does. hwin 0: 8 mean frames rounded up to a power of two (round 3);
+// 1: 4 mean frames or the sample's longest frame + 4 KiB, whichever is larger, in 4 KiB
+// steps. Both within [RW_HMIN, min(C / 2, RW_HMAX)].
+__device__ static u32 rw_window(u64 mean, u32 maxlen, u64 C, int hwin) {
+    const u64 hi = C / 2 < RW_HMAX ? C / 2 : RW_HMAX;
+    if (!hwin) return (u32)rw_pow2_clamp(mean * 8, RW_HMIN, hi);
+    u64 h = mean * 4 > (u64)maxlen + 4096 ? mean * 4 : (u64)maxlen + 4096;
+    h = (h + 4095) & ~4095ull;
+    return (u32)(h < RW_HMIN ? RW_HMIN : (h > hi ? hi : h));
+}
+
 struct RwRec {            // phase A: one surviving walk from chunk start + start
     u32 start;
     u32 cs;               // frames consumed | status << 31 (0 left the window, 1 the stream's walk ends)
@@ -495,7 +518,11 @@ __device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool
 // R1 (candidates): one thread per RW_TPOS window positions (aligned 16-B loads); the
 // plausible positions of a wavefront are appended to its chunk's list (capc slots) with
 // one atomic per wave on the chunk's counter
-// (lanes are dense in R2: a wrong start costs one lane-slot, not a wavefront-slot)
+// (lanes are dense in R2: a wrong start costs one lane-slot, not a wavefront-slot).
+// V: a candidate whose frame is followed by an implausible header inside its chunk is dropped
+// here (R2 would drop it at that step: its second header), so the list holds only starts that
+// survive two headers
+template <int V>
 __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
                                                          u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc,
@@ -547,6 +574,19 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         u64 rm = hi >= 64 ? ~0ull : (1ull << hi) - 1;
         rm &= lo >= 64 ? 0ull : ~0ull << lo;
         cands &= rm;
+        if (V) {
+            const u64 cend = cs0 + C;
+            u64 keep = cands;
+            while (cands) {
+                const u32 k = (u32)__builtin_ctzll(cands);
+                cands &= cands - 1;
+                u64 pos = p0 + k;
+                if (rw_step(origin, len, pos, need_mask) == 0 && pos < cend &&
+                    rw_step(origin, len, pos, need_mask) == 2)
+                    keep &= ~(1ull << k);
+            }
+            cands = keep;
+        }
     }
     const u32 n = (u32)__builtin_popcountll(cands);
     u32 incl = n;                                                            // wavefront inclusive scan
@@ -728,7 +768,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
-                                                        SdMirror* __restrict__ mirror) {
+                                                        SdMirror* __restrict__ mirror, int hwin) {
     const u32 lane = threadIdx.x;
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
     const int dev = fresh == 2;
@@ -751,7 +791,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     // the sample (a walk that ends in it finishes the stream: `out` given)
     const u64 send = len - P > RW_SAMPLE ? P + RW_SAMPLE : len;
     const SwOut o = stream_walk(buf, len, P, fresh ? 0 : sd->g, nf, send, false, max_frames, desc, items, ptr, pend,
-                                nwork, res, lane, plan->sample_out);
+                                nwork, res, lane, plan->sample_out, true);
     // the next call on this stream skips the pass rounds unless the sample looks like runs of
     // equal lengths (>= 3 frames and >= 4 per header round, the round that met the sample's end
     // not counted) or the stream ended in it
@@ -776,7 +816,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     u64 nch = (len - P1 + C - 1) / C;
     // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
     while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
-    const u32 H = (u32)rw_pow2_clamp(mean * 8, RW_HMIN, C / 2 < RW_HMAX ? C / 2 : RW_HMAX);
+    const u32 H = rw_window(mean, o.maxlen, C, hwin);
     u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
     while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
     u64 capc = H / 32;
@@ -1105,6 +1145,9 @@ WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long str
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
+WsOpt ws_stream_rw_h{1};        // "stream_rw_h": the chunk windows (rw_window) 1 from the sample's mean and
+                                // longest frame, 0 eight mean frames rounded up to a power of two
+WsOpt ws_stream_r1v{1};         // "stream_r1v": R1 checks each candidate's second header (0: R2 does)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
@@ -1212,7 +1255,8 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
         return ws_set_err("stream walk setup", e);
     const u32 need_mask = (hb[1] & 0x80u) ? 1u : 0u;
     const u64 threads = nchunks * (H / RW_TPOS);
-    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
+    auto r1 = ws_stream_r1v ? ws_rw_cand_kernel<1> : ws_rw_cand_kernel<0>;
+    hipLaunchKernelGGL(r1, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
                        (u32)nchunks, need_mask, cand, nrec, capc, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_cand_kernel launch", e);
     const u32 r2_blocks = (u32)std::min<u64>((nchunks * capc + 255) / 256, 4096);  // grid-stride
@@ -1344,9 +1388,10 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
-                       fresh, d_seg, Pw.disorder, mirror);
+                       fresh, d_seg, Pw.disorder, mirror, (int)ws_stream_rw_h);
     // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
-    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+    auto r1 = ws_stream_r1v ? ws_rw_cand_kernel<1> : ws_rw_cand_kernel<0>;
+    hipLaunchKernelGGL(r1, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        cand, nrec, 0u, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
