@@ -217,12 +217,10 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
  * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
- * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" / "stream_r1v" / "stream_rw_h" (raw stream:
+ * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:
  * chunk-parallel walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront;
  * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
- * call's chunk records linked in parallel 0/1, the candidate scan drops starts whose second
- * header is implausible 1, or leaves that to the window walks 0, each chunk's candidate window
- * 1 from the sample's mean and longest frame, 0 eight mean frames), "k2_timing" (see
+ * call's chunk records linked in parallel 0/1), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);

@@ -170,10 +170,10 @@ def test_stream_graph_replays_follow_the_walk_hint(dev):
     bytes change between replays (same length): every replay bit-exact vs the oracle"""
     mixed, *_ = wsynth.make_batch(1500, wsynth.PLEN_MIX3, 0, 0, 48)
     n = len(mixed)
-    uni, *_ = wsynth.make_batch(n // 4110 + 2, 0, 4096, 0, 5)
+    uni, *_ = wsynth.make_batch(n // 4000 + 2, 0, 4096, 0, 5)
     runs = np.concatenate([wsynth.make_batch(k, 0, fl, 0, 60 + i)[0]
                            for i, (k, fl) in enumerate([(4000, 125), (3000, 1500), (n // 65550 + 2, 65536)])])
-    mixed2, *_ = wsynth.make_batch(1600, wsynth.PLEN_MIX3, 0, 0, 49)
+    mixed2, *_ = wsynth.make_batch(2000, wsynth.PLEN_MIX3, 0, 0, 49)
     assert len(uni) >= n and len(runs) >= n and len(mixed2) >= n
     mf = 1 << 15
     d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)

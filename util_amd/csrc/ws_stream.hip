@@ -457,12 +457,12 @@ __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
 }
 
 // The window at each chunk's start must hold a frame start of the chain: any window longer
-// than every frame does. hwin 0: 8 mean frames rounded up to a power of two (round 3);
-// 1: 4 mean frames or the sample's longest frame + 4 KiB, whichever is larger, in 4 KiB
-// steps. Both within [RW_HMIN, min(C / 2, RW_HMAX)].
-__device__ static u32 rw_window(u64 mean, u32 maxlen, u64 C, int hwin) {
+// than every frame does. 4 mean frames or the sample's longest frame + 4 KiB, whichever is
+// larger, in 4 KiB steps, within [RW_HMIN, min(C / 2, RW_HMAX)] (round 3: 8 mean frames
+// rounded up to a power of two; cfg3 128 -> 92 KiB, stream 8.32-8.36 -> 8.19 ms eager,
+// profiles/r04_stream_rw_ab.log)
+__device__ static u32 rw_window(u64 mean, u32 maxlen, u64 C) {
     const u64 hi = C / 2 < RW_HMAX ? C / 2 : RW_HMAX;
-    if (!hwin) return (u32)rw_pow2_clamp(mean * 8, RW_HMIN, hi);
     u64 h = mean * 4 > (u64)maxlen + 4096 ? mean * 4 : (u64)maxlen + 4096;
     h = (h + 4095) & ~4095ull;
     return (u32)(h < RW_HMIN ? RW_HMIN : (h > hi ? hi : h));
@@ -519,10 +519,9 @@ __device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool
 // plausible positions of a wavefront are appended to its chunk's list (capc slots) with
 // one atomic per wave on the chunk's counter
 // (lanes are dense in R2: a wrong start costs one lane-slot, not a wavefront-slot).
-// V: a candidate whose frame is followed by an implausible header inside its chunk is dropped
+// A candidate whose frame is followed by an implausible header inside its chunk is dropped
 // here (R2 would drop it at that step: its second header), so the list holds only starts that
-// survive two headers
-template <int V>
+// survive two headers (cfg3: R2 150 -> 24 us, R1 + R2 279 -> 154 us with the windows below)
 __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
                                                          u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc,
@@ -574,7 +573,7 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         u64 rm = hi >= 64 ? ~0ull : (1ull << hi) - 1;
         rm &= lo >= 64 ? 0ull : ~0ull << lo;
         cands &= rm;
-        if (V) {
+        {
             const u64 cend = cs0 + C;
             u64 keep = cands;
             while (cands) {
@@ -768,7 +767,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
-                                                        SdMirror* __restrict__ mirror, int hwin) {
+                                                        SdMirror* __restrict__ mirror) {
     const u32 lane = threadIdx.x;
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
     const int dev = fresh == 2;
@@ -816,7 +815,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     u64 nch = (len - P1 + C - 1) / C;
     // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
     while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
-    const u32 H = rw_window(mean, o.maxlen, C, hwin);
+    const u32 H = rw_window(mean, o.maxlen, C);
     u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
     while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
     u64 capc = H / 32;
@@ -1145,9 +1144,6 @@ WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long str
 WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
-WsOpt ws_stream_rw_h{1};        // "stream_rw_h": the chunk windows (rw_window) 1 from the sample's mean and
-                                // longest frame, 0 eight mean frames rounded up to a power of two
-WsOpt ws_stream_r1v{1};         // "stream_r1v": R1 checks each candidate's second header (0: R2 does)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
@@ -1255,8 +1251,7 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
         return ws_set_err("stream walk setup", e);
     const u32 need_mask = (hb[1] & 0x80u) ? 1u : 0u;
     const u64 threads = nchunks * (H / RW_TPOS);
-    auto r1 = ws_stream_r1v ? ws_rw_cand_kernel<1> : ws_rw_cand_kernel<0>;
-    hipLaunchKernelGGL(r1, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
+    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
                        (u32)nchunks, need_mask, cand, nrec, capc, (const RwPlan*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_cand_kernel launch", e);
     const u32 r2_blocks = (u32)std::min<u64>((nchunks * capc + 255) / 256, 4096);  // grid-stride
@@ -1388,10 +1383,9 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
-                       fresh, d_seg, Pw.disorder, mirror, (int)ws_stream_rw_h);
+                       fresh, d_seg, Pw.disorder, mirror);
     // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
-    auto r1 = ws_stream_r1v ? ws_rw_cand_kernel<1> : ws_rw_cand_kernel<0>;
-    hipLaunchKernelGGL(r1, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        cand, nrec, 0u, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
