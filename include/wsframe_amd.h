@@ -192,11 +192,13 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
  * captured in a HIP graph: "stream_rounds" pass pairs (default 4), then, on a stream of
  * >= 512 KiB, the chunk-parallel walk below with its geometry chosen and its chunk records
  * linked on the device (scratch sized from len when captured: about 2-5 % of len), on a
- * shorter one a single wavefront. An eager call on a stream of >= 512 KiB reads the state back
- * after every such group of rounds (one small device-to-host copy, synchronizing
- * hip_stream): more rounds while they pay, and once lengths keep changing (>= 512 KiB and
- * >= 256 frames left) a chunk-parallel walk (speculative chunk entries, chunks of ~1024
- * mean frames up to 8 MiB, each written by one wavefront). Workspace and scratch are per
+ * shorter one a single wavefront. An eager call on a stream of >= 512 KiB waits for the state
+ * each round publishes to pinned host memory (no copy): more rounds while they pay, and once
+ * lengths keep changing (>= 512 KiB and >= 256 frames left) the chunk-parallel walk
+ * (speculative chunk entries, chunks of ~1024 mean frames up to 4 MiB by default, each written
+ * by one wavefront). While the previous chunk walk on the same stream (or the previous replay of
+ * a captured call) saw lengths that keep changing, the pass rounds are skipped and the walk
+ * starts at 0: results never depend on this. Workspace and scratch are per
  * (stream, graph capture), so calls on different streams may overlap. Returns 0 or a
  * negative error. */
 WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,

@@ -1141,7 +1141,8 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
 
 WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long streams, linked on the device
                                 // (1) or by the host (2, eager calls), 0 one wavefront
-WsOpt ws_stream_rw_cmax{23};    // "stream_rw_cmax": log2 of the largest chunk
+WsOpt ws_stream_rw_cmax{22};    // "stream_rw_cmax": log2 of the largest chunk (cfg3: 4 MiB 8.11-8.13 ms
+                                // against 8.19-8.21 at 8 MiB and 8.14-8.15 at 2 MiB, profiles/r04_stream_cmax_ab.log)
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
