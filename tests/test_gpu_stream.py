@@ -141,6 +141,35 @@ def test_long_stream_frames_longer_than_window(dev):
     assert int(r["consumed"]) == len(wire)
 
 
+def test_long_stream_rare_long_frames(dev):
+    """small frames with a rare 200-400 KiB one: the sample (first 256 KiB) rarely sees one, so
+    the chunk windows (from the sample's mean and longest frame) are far shorter than the frames
+    that cover some of them: those chunks are walked by one wavefront; eager and captured"""
+    def pick(g):
+        return int(g.integers(200 << 10, 400 << 10)) if g.random() < 0.004 else int(g.integers(0, 301))
+    wire = long_stream(np.random.default_rng(27), 24 << 20, pick)
+    r = run(dev, wire, 1 << 18)
+    assert int(r["consumed"]) == len(wire)
+    n = len(wire)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    desc = torch.zeros((1 << 18) * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(16, dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        W.stream_decode_device(d, n, 1 << 18, desc, res)
+    ob = wire.copy()
+    od, orr = oracle_segments(ob, [0], [n], 1 << 18)
+    for rnd in range(2):
+        d[:n].copy_(torch.from_numpy(wire).to(dev))
+        g.replay()
+        torch.cuda.synchronize()
+        gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+        assert tuple(gr) == tuple(orr[0]), rnd
+        assert np.array_equal(desc.cpu().numpy().view(W.DESC_DTYPE)[:int(gr["n_frames"])],
+                              od[:int(orr[0]["n_frames"])]), rnd
+        assert np.array_equal(d[:n].cpu().numpy(), ob), rnd
+
+
 def test_long_stream_unmasked_and_mixed(dev):
     """server frames (no MASK) and a stream that mixes both"""
     run(dev, long_stream(np.random.default_rng(24), 24 << 20, mix3, masked=0.0), 1 << 14)

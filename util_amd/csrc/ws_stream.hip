@@ -490,7 +490,18 @@ struct RwPlan {
     u32 H, nchunks, capc, stgn;
     u32 need_mask, active, nf, nrows;
     u64 sample_out[4];    // stream_walk's report of the sample / of a linked chunk walk
+    u32 seen_max, pad0;   // the longest frame the previous walk on this stream wrote (emit, linker)
 };
+
+// a wavefront's longest frame -> the plan's seen_max (the next call's windows cover it)
+__device__ __forceinline__ void rw_note_max(const RwPlan* plan, u32 mx, u32 lane) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const u32 o = (u32)__shfl_xor((int)mx, d);
+        mx = o > mx ? o : mx;
+    }
+    if (plan && lane == 0 && mx) atomicMax(const_cast<u32*>(&plan->seen_max), mx);
+}
 
 // b23: header bytes 2 and 3 (the top of a 64-bit length, which a real frame leaves zero:
 // a random 64-bit length reads as an incomplete frame and would crowd the records)
@@ -721,10 +732,14 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
     const bool last = t[6] != 0;
     const u32 lane = threadIdx.x;
     if (oi == ~0ull) {
-        stream_walk(buf, len, ent, 0, (u32)nf0, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
+        const SwOut o = stream_walk(buf, len, ent, 0, (u32)nf0, len, true, max_frames, desc, items, ptr, pend, nwork,
+                                    res, lane, nullptr, plan != nullptr);
+        rw_note_max(plan, o.maxlen, lane);
         return;
     }
-    stream_walk(buf, len, ent, 0, (u32)nf0, exit_w, false, max_frames, desc, items, ptr, pend, nwork, res, lane);
+    const SwOut o1 = stream_walk(buf, len, ent, 0, (u32)nf0, exit_w, false, max_frames, desc, items, ptr, pend, nwork,
+                                 res, lane, nullptr, plan != nullptr);
+    u32 mx = o1.maxlen;
     const RwOwn ow = own[oi];
     const u32* sl = stg + oi * stgn;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
@@ -736,6 +751,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
         u64 h0, h1;
         ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
         const WsHdr h = ws_parse(h0, h1, len - pos);                         // a frame (the owner walked it)
+        if ((u32)h.ret > mx) mx = (u32)h.ret;
         const u64 slot = nf0 + cnt_w + i;
         const u64 fo = lead0 + pos, p0 = fo + h.hdr, fe = p0 + h.plen;
         const u64 w0 = p0 | ((u64)(rotl32(h.key, 8u * (u32)(p0 & 3)) & 0xFFFFu) << 48);
@@ -750,8 +766,9 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
     const u64 nb = ow.cs & 0x7FFFFFFFu;
     const u64 staged = nb < stgn ? nb : stgn;
     const u64 next = n_par < staged ? cs0 + sl[n_par] : (n_par == nb ? ow.exit : ow.over);
-    stream_walk(buf, len, next, 0, (u32)(nf0 + cnt_w + n_par), last ? len : ow.exit, last, max_frames, desc, items,
-                ptr, pend, nwork, res, lane);
+    const SwOut o2 = stream_walk(buf, len, next, 0, (u32)(nf0 + cnt_w + n_par), last ? len : ow.exit, last, max_frames,
+                                 desc, items, ptr, pend, nwork, res, lane, nullptr, plan != nullptr);
+    rw_note_max(plan, o2.maxlen > mx ? o2.maxlen : mx, lane);
 }
 
 // ---- the chunk-parallel walk inside a captured call (no host reads): the plan kernel
@@ -769,6 +786,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
                                                         SdMirror* __restrict__ mirror) {
     const u32 lane = threadIdx.x;
+    const u32 seen = plan->seen_max;        // the previous walk's longest frame (garbage before the first)
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
     const int dev = fresh == 2;
     if (dev) fresh = sd->walk_hint != 0;
@@ -815,7 +833,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     u64 nch = (len - P1 + C - 1) / C;
     // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
     while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
-    const u32 H = rw_window(mean, o.maxlen, C);
+    const u32 H = rw_window(mean, o.maxlen > seen ? o.maxlen : seen, C);
     u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
     while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
     u64 capc = H / 32;
@@ -830,6 +848,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
         plan->need_mask = (buf[P1 + 1] & 0x80u) ? 1u : 0u;                   // client frames: masked
         plan->nf = o.nf;
         plan->nrows = 0;
+        plan->seen_max = 0;                 // this call's emit and linker fill it in
         plan->active = 1;
     }
 }
@@ -1035,7 +1054,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     // moves to the next chunk), then taken one chunk at a time; a chain that leaves that run
     // (a skipped chunk, a chunk walked here) reloads at its new chunk.
     constexpr u32 RW_LK = 8;
-    u32 steps = 0;
+    u32 steps = 0, mx = 0;
     while (!last && ent < len && steps <= nchunks + 1) {
         const u64 c0 = (ent - P) / C;
         // lane l < RW_LK: the record counts of chunk c0 + l (read back per chunk by readlane)
@@ -1126,7 +1145,8 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
             }
             // no usable record: this wavefront walks the chunk (writing its frames)
             const SwOut o = stream_walk(buf, len, ent, 0, nfc, cs0 + C < len ? cs0 + C : len, false, max_frames, desc,
-                                        items, ptr, pend, nwork, res, lane, plan->sample_out);
+                                        items, ptr, pend, nwork, res, lane, plan->sample_out, true);
+            if (o.maxlen > mx) mx = o.maxlen;
             if (o.ended) { last = true; break; }                            // (the walk finished the stream)
             if (o.next <= ent) { steps = nchunks + 2; break; }               // (cannot happen: no progress)
             ent = o.next;
@@ -1134,8 +1154,12 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
             reload = true;                                                   // its frames may cross chunks
         }
     }
-    if (!last)                                                               // safety: walk whatever is left
-        stream_walk(buf, len, ent, 0, nfc, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
+    if (!last) {                                                             // safety: walk whatever is left
+        const SwOut o = stream_walk(buf, len, ent, 0, nfc, len, true, max_frames, desc, items, ptr, pend, nwork, res,
+                                    lane, nullptr, true);
+        if (o.maxlen > mx) mx = o.maxlen;
+    }
+    rw_note_max(plan, mx, lane);
     if (lane == 0) plan->nrows = rows;
 }
 
