@@ -14,6 +14,8 @@
 //   13 K1 + plain XOR of `arg` MiB of another buffer + K2   14 read the workspace (items, pointers) + K2
 //   15 K1 twice + K2
 //   11 latency-bound chase kernel (arg % 1000 x 10 us; 256 blocks if arg > 1000, else 1) + K2   12 it alone
+//   20-23 a pass of arg MiB over another buffer + K2 (20 nt XOR, 21 plain write-only, 22 nt
+//   write-only, 23 plain read-only); 30-33 the same pass alone
 #include "../util_amd/csrc/ws_common.h"
 
 __global__ void exp_spin_kernel(unsigned long long ticks) {
@@ -42,6 +44,32 @@ __global__ __launch_bounds__(256) void exp_xor_kernel(gu32x4* __restrict__ a, un
         v.x ^= 0x5A5A5A5Au; v.y ^= 0x5A5A5A5Au; v.z ^= 0x5A5A5A5Au; v.w ^= 0x5A5A5A5Au;
         a[i] = v;
     }
+}
+
+// passes over n16 16-B chunks of another buffer, by cache policy (round 4: what in a pass in
+// front of K2 makes it fast): 0 nt XOR (nt loads + nt stores), 1 plain write-only, 2 nt
+// write-only, 3 plain read-only
+template <int KIND>
+__global__ __launch_bounds__(256) void exp_pass_kernel(gu32x4* __restrict__ a, unsigned long long n16, u32* sink) {
+    u32 h = 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n16;
+         i += (unsigned long long)gridDim.x * 256) {
+        if (KIND == 0) {
+            u32x4 v = __builtin_nontemporal_load(a + i);
+            v.x ^= 0x5A5A5A5Au; v.y ^= 0x5A5A5A5Au; v.z ^= 0x5A5A5A5Au; v.w ^= 0x5A5A5A5Au;
+            __builtin_nontemporal_store(v, a + i);
+        } else if (KIND == 1) {
+            const u32x4 v = {(u32)i, 1u, 2u, 3u};
+            a[i] = v;
+        } else if (KIND == 2) {
+            const u32x4 v = {(u32)i, 1u, 2u, 3u};
+            __builtin_nontemporal_store(v, a + i);
+        } else {
+            const u32x4 v = a[i];
+            h ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (KIND == 3 && h == 0xA5A5F00Du) *gptr<u32>(sink) = h;
 }
 
 // read every 16-B entry of [p, p + n16) (the items / piece pointers K2 will read)
@@ -154,9 +182,21 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
             if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
             break;
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
+        case 20: case 30: case 21: case 31: case 22: case 32: case 23: case 33: {   // pass of arg MiB (+ K2 for 2x)
+            gu32x4* o = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(other));
+            const unsigned long long n16 = (unsigned long long)arg << 16;
+            const int kind = mode % 10;
+            if (kind == 0) hipLaunchKernelGGL(exp_pass_kernel<0>, dim3(4096), dim3(256), 0, st, o, n16, sink);
+            if (kind == 1) hipLaunchKernelGGL(exp_pass_kernel<1>, dim3(4096), dim3(256), 0, st, o, n16, sink);
+            if (kind == 2) hipLaunchKernelGGL(exp_pass_kernel<2>, dim3(4096), dim3(256), 0, st, o, n16, sink);
+            if (kind == 3) hipLaunchKernelGGL(exp_pass_kernel<3>, dim3(4096), dim3(256), 0, st, o, n16, sink);
+            break;
+        }
         default: break;
         }
-        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16) || mode == 18) && (rc = ws_launch_piece_unmask(L, P, gen))) return rc;
+        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16) || mode == 18 || (mode >= 20 && mode <= 23)) &&
+            (rc = ws_launch_piece_unmask(L, P, gen)))
+            return rc;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -28,7 +28,8 @@ st = torch.cuda.current_stream()
 nframes = wl.nframes
 stride = int(os.environ.get("EXP_STRIDE", "4104"))
 names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
-         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase", 13: "K1+xor+K2", 14: "wsread+K2", 15: "K1K1+K2", 16: "alu+K2", 17: "alu", 18: "xor+K2", 19: "xor"}
+         6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase", 13: "K1+xor+K2", 14: "wsread+K2", 15: "K1K1+K2", 16: "alu+K2", 17: "alu", 18: "xor+K2", 19: "xor",
+         20: "ntxor+K2", 21: "wr+K2", 22: "ntwr+K2", 23: "rd+K2", 30: "ntxor", 31: "wr", 32: "ntwr", 33: "rd"}
 seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
 if os.environ.get("EXP_MODES"):
     seq = [tuple(int(y) for y in x.split(":")) for x in os.environ["EXP_MODES"].split(",")]
