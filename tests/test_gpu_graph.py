@@ -335,3 +335,85 @@ def test_capture_only_process_reuses_dead_slots(dev, kind):
     for _ in range(30):
         cycle()
     assert W.get_stat("workspace_bytes") <= base, (base, W.get_stat("workspace_bytes"))
+
+
+@pytest.mark.parametrize("path", [1, 2], ids=["fused", "three_kernel"])
+def test_reassemble_graph_replay(dev, path):
+    """websocketframeBatchReassembleDeviceEx captured in a graph (fused kernel, or scan +
+    layout + gather with its workspace): two replays, each bit-exact vs the oracle (the wire is
+    only read, so the same inputs give the same outputs)"""
+    from oracle_lib import oracle_reassemble, used_descs
+    rng = np.random.default_rng(61)
+    wire, so, sl = random_stream(rng, 500)
+    mf = 16
+    n, nseg = len(wire), len(so)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    d[:n] = torch.from_numpy(wire).to(dev)
+    T = lambda a: torch.tensor(np.asarray(a, dtype=np.int64), device=dev)  # noqa: E731
+    so_t, sl_t = T(so), T(sl)
+    out = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(nseg * mf * 32, dtype=torch.uint8, device=dev)
+    msg = torch.zeros(nseg * mf * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(nseg * 16, dtype=torch.uint8, device=dev)
+    nmsg = torch.zeros(nseg, dtype=torch.int32, device=dev)
+    od, orr, oms, oreg, _, _ = oracle_reassemble(wire, so, sl, mf)
+    W.set_option("reasm_path", path)
+    try:
+        W.batch_reassemble_device(d, so_t, sl_t, mf, desc, res, out, msg, nmsg)   # workspace exists from here
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            W.batch_reassemble_device(d, so_t, sl_t, mf, desc, res, out, msg, nmsg)
+    finally:
+        W.set_option("reasm_path", 0)
+    for rnd in range(2):
+        for t in (out, desc, msg, res, nmsg):
+            t.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        gr = res.cpu().numpy().view(W.SEGRES_DTYPE)
+        assert np.array_equal(gr, orr), rnd
+        gd = desc.cpu().numpy().view(W.DESC_DTYPE)
+        assert np.array_equal(used_descs(gd, gr, mf), used_descs(od, orr, mf)), rnd
+        gm, gn, ob_all = msg.cpu().numpy().view(W.MSG_DTYPE), nmsg.cpu().numpy(), out.cpu().numpy()
+        for s in range(nseg):
+            assert int(gn[s]) == len(oms[s]), (rnd, s)
+            for i, m in enumerate(oms[s]):
+                assert tuple(int(gm[s * mf + i][f]) for f in W.MSG_DTYPE.names) == m, (rnd, s, i)
+            ob, body = oreg[s]
+            assert np.array_equal(ob_all[ob:ob + len(body)], body), (rnd, s)
+        assert np.array_equal(d[:n].cpu().numpy(), wire), rnd
+
+
+@pytest.mark.parametrize("front", [1, 0], ids=["front", "hipcub"])
+def test_encode_graph_replay(dev, front):
+    """websocketframeBatchEncodeDevice captured in a graph (both fronts): two replays into a
+    cleared buffer, each bit-exact vs the oracle composition"""
+    from oracle_lib import oracle_encode_frames
+    from test_gpu_encode import random_frames
+    rng = np.random.default_rng(62)
+    src, fr = random_frames(rng, 600)
+    want, woff = oracle_encode_frames(src, fr)
+    s = torch.from_numpy(src).to(dev)
+    f = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+    cap = int(fr["len"].sum()) + 14 * len(fr)
+    dst = torch.zeros(cap + 64, dtype=torch.uint8, device=dev)
+    off = torch.zeros(len(fr) + 1, dtype=torch.int64, device=dev)
+    W.set_option("enc_front", front)
+    try:
+        W.batch_encode_device(s, f, dst[:cap], off, capacity=cap)              # workspace exists from here
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            W.batch_encode_device(s, f, dst[:cap], off, capacity=cap)
+    finally:
+        W.set_option("enc_front", 1)
+    for rnd in range(2):
+        dst.fill_(0xA5)
+        off.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(off.cpu().numpy().astype(np.uint64), woff), rnd
+        got = dst.cpu().numpy()
+        assert np.array_equal(got[:len(want)], np.frombuffer(want, dtype=np.uint8)), rnd
+        assert (got[len(want):] == 0xA5).all(), rnd
