@@ -279,3 +279,49 @@ def test_stream_skips_rounds_while_lengths_keep_changing(dev):
         skipped = W.get_stat("stream_skips") == n0 + 1
         if want is not None:
             assert skipped == want, (i, skipped)
+
+
+def test_two_raw_streams_in_parallel_threads(dev):
+    """two host threads, each decoding its own raw stream on its own HIP stream, four calls each:
+    every HIP stream has its own workspace, pass state and walk hint (one thread's changing
+    stream must not make the other's uniform stream skip its rounds, or the reverse); every call
+    bit-exact vs the oracle"""
+    import threading
+    mixed, *_ = wsynth.make_batch(1500, wsynth.PLEN_MIX3, 0, 0, 71)
+    uni, *_ = wsynth.make_batch(9000, 0, 4096, 0, 72)
+    mixed2, *_ = wsynth.make_batch(1400, wsynth.PLEN_MIX3, 0, 0, 73)
+    plans = {0: [mixed, mixed, uni, mixed2], 1: [uni, uni, mixed2, uni]}
+    want = {}
+    for w in (mixed, uni, mixed2):
+        ob = w.copy()
+        od, orr = oracle_segments(ob, [0], [len(w)], 1 << 15)
+        want[id(w)] = (ob, od[:int(orr[0]["n_frames"])], tuple(orr[0]))
+    errors = []
+
+    def worker(k):
+        try:
+            st = torch.cuda.Stream(dev)
+            cap = max(len(w) for w in plans[k]) + 64
+            d = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            desc = torch.zeros((1 << 15) * 32, dtype=torch.uint8, device=dev)
+            res = torch.zeros(16, dtype=torch.uint8, device=dev)
+            for i, w in enumerate(plans[k]):
+                with torch.cuda.stream(st):
+                    d[:len(w)].copy_(torch.from_numpy(w).to(dev, non_blocking=False))
+                    W.stream_decode_device(d, len(w), 1 << 15, desc, res, stream=st)
+                st.synchronize()
+                ob, od, orr = want[id(w)]
+                gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+                assert tuple(gr) == orr, (k, i)
+                assert np.array_equal(desc.cpu().numpy().view(W.DESC_DTYPE)[:len(od)], od), (k, i)
+                assert np.array_equal(d[:len(w)].cpu().numpy(), ob), (k, i)
+        except BaseException as e:  # noqa: BLE001 - reported by the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), "a decode thread hung"
+    assert not errors, errors
