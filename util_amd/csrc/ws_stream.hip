@@ -150,7 +150,10 @@ __global__ __launch_bounds__(SPASS_T) void ws_stream_pass_kernel(const unsigned 
 }
 
 // Frames of the stream starting in [P0, end) from (P0, nf0, g0) by one wavefront: the group
-// walk of ws_piece.hip (64 lanes, stride speculation; only consumed frames are written).
+// walk of ws_piece.hip (stride speculation; only consumed frames are written). The
+// speculative width adapts: 64 lanes while runs of equal lengths hold, 2 (k + 1) lanes after a
+// length change at lane k (at least 4), doubling after every step whose lanes all confirmed —
+// on lengths that change every frame a step loads 4 header lines instead of 64.
 // `last`: the walk runs to the stream's end (end == len) and then writes the tail
 // pointers, the item count and the segment result; otherwise it stops before the first
 // frame starting at or after `end` (another wavefront owns it).
@@ -171,11 +174,12 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
     u32 nf = nf0, extra = 0;
     int status = WEBSOCKET_SEG_OK;
     bool at_bnd = false;
-    u32 steps = 0, mx = 0;
+    u32 steps = 0, mx = 0, w = 64;
     for (;;) {
         ++steps;
+        const u32 wl = g > 0 ? w : 1u;                                      // lanes evaluated
         const u64 pos = off + (u64)lane * g;
-        const bool cand = lane == 0 || g > 0;
+        const bool cand = lane < wl;
         const bool eval = cand && pos < len;
         const uintptr_t pa = seg + (eval ? pos : 0);
         const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
@@ -194,9 +198,9 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
             else if (h.ret <= 0) { code = 2; st = h.ret < 0 ? WEBSOCKET_SEG_ERR_DECODE : WEBSOCKET_SEG_OK; }
             else code = (u64)(u32)h.ret == g ? 0u : 1u;
         }
-        const u64 stopm = __ballot(code != 0);
-        const u32 mm = stopm ? (u32)__builtin_ctzll(stopm) : 64u;
-        const u32 code_m = mm < 64 ? (u32)__builtin_amdgcn_readlane((int)code, (int)mm) : 0u;
+        const u64 stopm = __ballot(cand && code != 0);
+        const u32 mm = stopm ? (u32)__builtin_ctzll(stopm) : wl;
+        const u32 code_m = stopm ? (u32)__builtin_amdgcn_readlane((int)code, (int)mm) : 0u;
         const u32 ntake = mm + ((code_m == 1 || code_m == 2) ? 1u : 0u);
         const u64 fo = lead0 + pos, p0 = fo + h.hdr, fe = p0 + h.plen;
         if (lane < ntake) {
@@ -211,11 +215,22 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
         }
         if (ntake) walked_end = __shfl(fe, (int)ntake - 1);
         if (want_max && lane < ntake && h.ret > 0 && (u32)h.ret > mx) mx = (u32)h.ret;
-        if (mm == 64) { nf += 64; off += 64 * g; continue; }
+        if (!stopm) {                                                        // every evaluated lane confirmed
+            nf += wl;
+            off += (u64)wl * g;
+            w = w < 32 ? 2 * w : 64;
+            continue;
+        }
         const u64 pos_m = off + (u64)mm * g;
         const int ret_m = __builtin_amdgcn_readlane(h.ret, (int)mm);
         nf += mm;
-        if (code_m == 1) { nf += 1; off = pos_m + (u32)ret_m; g = (u32)ret_m; continue; }
+        if (code_m == 1) {                                                   // (g 0: the first frame, no history)
+            nf += 1;
+            off = pos_m + (u32)ret_m;
+            w = g == 0 ? 64u : (mm < 2 ? 4u : (mm < 32 ? 2 * (mm + 1) : 64u));
+            g = (u32)ret_m;
+            continue;
+        }
         off = pos_m;
         at_bnd = __builtin_amdgcn_readlane((int)bnd, (int)mm) != 0;
         if (code_m == 2) {
