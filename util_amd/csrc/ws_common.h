@@ -34,10 +34,11 @@ __device__ __forceinline__ WS_GLOBAL T* gptr(const void* p) {
     return reinterpret_cast<WS_GLOBAL T*>(reinterpret_cast<uintptr_t>(p));
 }
 
-// Cache policy of the payload stream (A/B-able): 0 plain, 1 nontemporal loads+stores, 2 nt stores.
+// Cache policy of the payload stream (A/B-able): 0 plain, 1 nontemporal loads+stores, 2 nt stores,
+// 4 nontemporal loads + the caller's own sc1|nt buffer stores (st16<4> is an nt store).
 template <int NT>
 __device__ __forceinline__ u32x4 ld16(const gu32x4* p) {
-    if constexpr (NT == 1) return __builtin_nontemporal_load(p);
+    if constexpr (NT == 1 || NT == 4) return __builtin_nontemporal_load(p);
     else return *p;
 }
 #ifndef WS_ST16_PLAIN

@@ -323,8 +323,9 @@ __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(WalkArgs A, u32*
 
 // K2. Kept configuration (the A/B variants of rounds 1-2 are gone: plain loads/stores,
 // exact-byte-only or one-segment whole stores, forced 7-8 waves/SIMD, other window maps —
-// all measured slower): nontemporal loads and stores, chunks wholly inside
-// segments stored whole (byte coverage by the visited segments), 2^wshift windows.
+// all measured slower): nontemporal loads, nontemporal system-coherent (sc1)
+// whole-chunk stores (NT 4), chunks wholly inside segments stored whole (byte coverage by the
+// visited segments), 2^wshift windows.
 template <int NT, int SR>
 __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char* __restrict__ buf,
                                                                   const u64* __restrict__ seg_off,
@@ -459,13 +460,25 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     }
     // ---- 3. store (v[] holds the unmasked bytes): full chunks one 16-B store, edge chunks
     //         exactly the covered bytes
+    // NT 4: whole chunks leave as `buffer_store_dwordx4 … nt sc1` through a descriptor over this
+    // wave's 4 KiB (round 4: −0.15–0.5 % per step against `global_store … nt` on cfg2, cfg3 and
+    // the raw stream, `profiles/r04_k2_store_sc1nt_ab.log`; a one-shot XOR block streams 2.6 %
+    // faster that way, `profiles/r04_calib_store_policy.log`)
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t wrs;
+    if constexpr (NT == 4)
+        wrs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(base + wc0)),
+                                                (short)0, 64 * PIECE_U * 16, 0x00020000);
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) {
         const u64 c = wc0 + (u64)(u * 64 + lane);
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         const u32x4 w = v[u];
         if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
-            st16<NT>(w, base + c);
+            if constexpr (NT == 4)                                           // sc1 | nt
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, w),
+                                                       wrs, (int)((u * 64 + lane) * 16), 0, 18);
+            else
+                st16<NT>(w, base + c);
         } else {
             ws_store_bytes(reinterpret_cast<gu8*>(base + c), w, cov[u]);
         }
@@ -622,12 +635,12 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
     if (P.segr)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)P.segr);
     else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<1, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)nullptr);
