@@ -50,6 +50,16 @@ __device__ __forceinline__ void st16(u32x4 v, gu32x4* p) {
     else *p = v;
 }
 
+// A wave-uniform buffer descriptor over `bytes` from p, for `buffer_store_dwordx4 … nt sc1`
+// stores at per-lane offsets (stores outside [0, bytes) are dropped by the hardware)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(uintptr_t p, u32 bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1nt(u32x4 v, __amdgpu_buffer_rsrc_t r, u32 off) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
+                                           (int)off, 0, 18);
+}
+
 __device__ __forceinline__ u32 rotl32(u32 x, u32 r) { return r ? (x << r) | (x >> (32 - r)) : x; }
 
 // Result of parsing one frame header (websocketframe.c:112-165).

@@ -329,6 +329,8 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
         v[u] = (u32x4){0, 0, 0, 0};
         if (kind[u] == 1) v[u] = *reinterpret_cast<const WS_GLOBAL u32x4u*>(reinterpret_cast<uintptr_t>(src + fsrc[u]));
     }
+    // (nt stores: sc1|nt measured +5 %, profiles/r04_store_sc1nt_ab.log — unlike the in-place
+    // decode kernels, where it gains)
 #pragma unroll
     for (int u = 0; u < ENC_U; ++u) {
         const u64 x = r0 + (u64)(u * 1024 + lane * 16);

@@ -465,18 +465,14 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     // the raw stream, `profiles/r04_k2_store_sc1nt_ab.log`; a one-shot XOR block streams 2.6 %
     // faster that way, `profiles/r04_calib_store_policy.log`)
     [[maybe_unused]] __amdgpu_buffer_rsrc_t wrs;
-    if constexpr (NT == 4)
-        wrs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(base + wc0)),
-                                                (short)0, 64 * PIECE_U * 16, 0x00020000);
+    if constexpr (NT == 4) wrs = ws_rsrc(reinterpret_cast<uintptr_t>(base + wc0), 64 * PIECE_U * 16);
 #pragma unroll
     for (int u = 0; u < PIECE_U; ++u) {
         const u64 c = wc0 + (u64)(u * 64 + lane);
         if (!cov[u] || c < c_lo || c >= c_hi) continue;
         const u32x4 w = v[u];
         if (cov[u] == 0xFFFFu || segcov[u] == 0xFFFFu) {
-            if constexpr (NT == 4)                                           // sc1 | nt
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, w),
-                                                       wrs, (int)((u * 64 + lane) * 16), 0, 18);
+            if constexpr (NT == 4) st16_sc1nt(w, wrs, (u * 64 + lane) * 16);
             else
                 st16<NT>(w, base + c);
         } else {

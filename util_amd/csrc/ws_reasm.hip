@@ -281,9 +281,12 @@ struct BodyL {           // body table entry (LDS; its key, rotated to the absol
 // o0 & 15 is the same for every chunk of the body (wave-uniform), so the 16 bytes are four
 // v_alignbyte_b32 of dwords picked at compile time (SD = (o0 >> 2) & 3, one loop per SD),
 // not a per-lane 64-bit funnel shift.
+// Stores: sc1|nt through a descriptor over the body (cfg5 1.403-1.406 -> 1.392-1.399 ms against
+// nt global stores, profiles/r04_store_sc1nt_ab.log).
 template <int SD>
 __device__ __forceinline__ void reasm_copy(const u32x4* win, u32 o0, u32 nch, u32 key, u64 dst, u32 lane) {
     const u32 sb = o0 & 3u;
+    const __amdgpu_buffer_rsrc_t wrs = ws_rsrc((uintptr_t)dst, nch * 16u);
     for (u32 c = lane; c < nch; c += 64) {
         const u32 i = (o0 >> 4) + c;
         const u32x4 a = win[i], b = win[i + 1];
@@ -293,7 +296,7 @@ __device__ __forceinline__ void reasm_copy(const u32x4* win, u32 o0, u32 nch, u3
         w.y = __builtin_amdgcn_alignbyte(d[SD + 2], d[SD + 1], sb) ^ key;
         w.z = __builtin_amdgcn_alignbyte(d[SD + 3], d[SD + 2], sb) ^ key;
         w.w = __builtin_amdgcn_alignbyte(d[SD + 4], d[SD + 3], sb) ^ key;
-        st16<1>(w, reinterpret_cast<gu32x4*>(dst + ((u64)c << 4)));
+        st16_sc1nt(w, wrs, c << 4);
     }
 }
 

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
             if (c0 > cmax) break;
             const u64 c = c0 + lane < cmax ? c0 + lane : cmax;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const WS_GLOBAL void*>(gseg + c),
-                                             (lds_void*)(&win[i * 64]), 16, 0, NT == 1 ? 2 : 0);
+                                             (lds_void*)(&win[i * 64]), 16, 0, NT == 1 || NT == 4 ? 2 : 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -142,8 +142,11 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
             u32x4 w = win[cb + lane];
             w.x ^= m0; w.y ^= m1; w.z ^= m2; w.w ^= m3;
             gu32x4* const pc = gseg + (wc + cb + lane);
-            if (x >= xseg0 && x + 16 <= xseg1) {
-                st16<NT>(w, pc);                                         // whole chunk inside the segment
+            if (x >= xseg0 && x + 16 <= xseg1) {                         // whole chunk inside the segment
+                // NT 4: sc1|nt through a descriptor over the wave's 1 KiB row (cfg5 1.386-1.388 ->
+                // 1.368-1.373 ms against nt stores, profiles/r04_store_sc1nt_ab.log)
+                if constexpr (NT == 4) st16_sc1nt(w, ws_rsrc(reinterpret_cast<uintptr_t>(gseg + (wc + cb)), 1024), lane * 16);
+                else st16<NT>(w, pc);
             } else {
                 ws_store_bytes(reinterpret_cast<gu8*>(pc), w, cov);
             }
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
 int ws_launch_segfuse(const WsLaunch& L) {
     if (L.max_frames > SF_TB) return ws_set_msg("segfuse path: max_frames > 64");
     const u32 half = ws_seg_win && L.nseg >= 512 ? (L.nseg + 1) / 2 : 0;
-    hipLaunchKernelGGL((ws_segfuse_kernel<1, 18, 256>), dim3(half ? 2 * half : L.nseg), dim3(256), 0, L.stream, L.buf,
+    hipLaunchKernelGGL((ws_segfuse_kernel<4, 18, 256>), dim3(half ? 2 * half : L.nseg), dim3(256), 0, L.stream, L.buf,
                        L.seg_off, L.seg_len, L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_segfuse_kernel launch", e);
