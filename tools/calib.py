@@ -29,7 +29,8 @@ def main():
         names = {16: "buf256x4_nt_nt", 17: "buf256x4_plain", 18: "buf256x4_nt_sc1", 19: "buf256x4_nt_plain",
                  20: "buf256x4_plain_nt", 21: "buf256x8_nt", 22: "buf512x4_nt", 23: "buf1024x4_nt",
                  24: "buf256x2_nt", 25: "buf256x16_nt", 26: "buf256x4_sc0nt", 27: "buf256x4_nt_sc1nt",
-                 28: "buf128x4_nt", 29: "buf64x4_nt", 5: "rounds1", 4: "oneshot",
+                 28: "buf128x4_nt", 29: "buf64x4_nt", 30: "buf256x4_sc1nt_sc1nt", 31: "buf256x4_sc0nt_sc1nt",
+                 32: "buf256x4_sc0sc1nt_sc1nt", 33: "buf256x4_sc1_sc1nt", 34: "buf256x4_nt_sc0sc1nt", 5: "rounds1", 4: "oneshot",
                  40: "ldspipe512x6_c3", 41: "ldspipe512x8_c3", 42: "ldspipe256x12_c3", 43: "ldspipe1024x3_c3",
                  44: "ldspipe512x6_c1", 45: "ldspipe512x6_c7", 46: "ldspipe256x8_c3", 47: "ldspipe512x6_il",
                  48: "ldspipe256x8_il", 49: "ldspipe1024x3_il", 60: "dep256x4_d0", 61: "dep256x4_d1",

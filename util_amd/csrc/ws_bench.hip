@@ -844,6 +844,11 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuCalibrate(void* d_a, void* d_
         case 27: cal_buf<256, 4, 2, 18>(a8, nb, st); break;
         case 28: cal_buf<128, 4, 2, 2>(a8, nb, st); break;
         case 29: cal_buf<64, 4, 2, 2>(a8, nb, st); break;
+        case 30: cal_buf<256, 4, 18, 18>(a8, nb, st); break;   // sc1|nt loads, sc1|nt stores
+        case 31: cal_buf<256, 4, 3, 18>(a8, nb, st); break;    // sc0|nt loads, sc1|nt stores
+        case 32: cal_buf<256, 4, 19, 18>(a8, nb, st); break;   // sc0|sc1|nt loads, sc1|nt stores
+        case 33: cal_buf<256, 4, 16, 18>(a8, nb, st); break;   // sc1 loads, sc1|nt stores
+        case 34: cal_buf<256, 4, 2, 19>(a8, nb, st); break;    // nt loads, sc0|sc1|nt stores
         default: return ws_set_msg("websocketframeGpuCalibrate: unknown mode");
         }
         hipError_t e = hipGetLastError();
