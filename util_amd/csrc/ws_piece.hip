@@ -554,19 +554,22 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 }
 
 // "piece_lds": bytes of unused dynamic LDS per K2 block, which caps its
-// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 6 — K2 needs only 60 VGPRs
-// (8 waves/SIMD would fit) but streams best at 6 blocks per CU in round 3 (cfg2 K1 + K2
-// 1.355 ms at 6 against 1.375-1.378 at 4 and 5, 1.374 at 7, 1.40 at 8, interleaved in one
-// process on three boxes: profiles/r03_k2_occupancy.log; round 2's K2 was best at 5). On
-// gfx950 (160 KiB per CU) that is 27,136 B.
+// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 7 when the batch holds at
+// least one segment per 8 pieces, else / 6. K2 needs only 60 VGPRs (8 waves/SIMD would fit);
+// with nontemporal stores it streamed best at 6 blocks per CU (round 3: cfg2 K1 + K2 1.355 ms
+// at 6 against 1.375-1.378 at 4 and 5, 1.374 at 7, profiles/r03_k2_occupancy.log); with the
+// sc1|nt stores (round 4) batches dense in segments (cfg2: 1 per 4 pieces, a wave's item and
+// segment lookups take longer) gain a seventh block (cfg2 -0.45-0.7 % on two boxes), while
+// large-frame batches (cfg3 1 per 44 pieces, cfg4 1 per 64) keep 6 (+0.6-0.75 % at 7;
+// profiles/r04_k2_occupancy_sc1.log). gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
-int ws_piece_dyn_lds(const WsLaunch& L) {
+int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces) {
     const int opt = ws_piece_lds;
     if (opt > 0) return opt <= 65536 ? opt : 65536;
-    const int per = L.lds_per_cu / 6;                       // 6 blocks per CU
+    const int per = L.lds_per_cu / ((u64)L.nseg * 8 >= npieces ? 7 : 6);   // 7 or 6 blocks per CU
     return per > 65536 ? 65536 : (per & ~255);
 }
 
@@ -631,12 +634,12 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
     if (P.segr)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)P.segr);
     else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)nullptr);
