@@ -398,8 +398,8 @@ struct PieceWs {          // ws_piece.hip workspace views after K1
 };
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
                          bool count_nonuniform = false, u32 g0 = 0);
-int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr);
-int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces);
+int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr, u32 g0 = 0);
+int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0 = 0);
 u32 ws_next_gen();
 int ws_device_info(int* cus, int* lds_per_cu);
 // auxiliary workspace: device scratch whose first WS_AUX_HEAD bytes are zero at allocation +

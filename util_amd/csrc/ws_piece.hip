@@ -566,10 +566,14 @@ WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
 
-int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces) {
+int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0) {
     const int opt = ws_piece_lds;
     if (opt > 0) return opt <= 65536 ? opt : 65536;
-    const int per = L.lds_per_cu / ((u64)L.nseg * 8 >= npieces ? 7 : 6);   // 7 or 6 blocks per CU
+    // 7 blocks per CU for frames of <= 16 KiB (several per piece), 6 for larger ones; the frame
+    // length is the previous call's advice when it had frames of one length (g0), else the
+    // batch's segment density stands in for it
+    const bool seven = g0 >= 2 ? g0 <= 16384u : (u64)L.nseg * 8 >= npieces;
+    const int per = L.lds_per_cu / (seven ? 7 : 6);
     return per > 65536 ? 65536 : (per & ~255);
 }
 
@@ -624,7 +628,7 @@ static u32 piece_wshift(u64 npieces) {
 
 // K2 over the pieces of a scanned batch; advice (device view of pinned host memory, may be
 // null): K2 turns K1's non-uniform count into the host's stride hint for the next call
-int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice) {
+int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice, u32 g0) {
     if (!P.npieces) return 0;
     size_t tslot = 0;
     int rc;
@@ -634,12 +638,12 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
     if (P.segr)
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)P.segr);
     else
-        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces), L.stream,
+        hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)nullptr);
@@ -655,7 +659,7 @@ int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 ge
     PieceWs P;
     int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr, g0);
     if (rc) return rc;
-    if ((rc = ws_launch_piece_unmask(L, P, gen, advice))) return rc;
+    if ((rc = ws_launch_piece_unmask(L, P, gen, advice, g0))) return rc;
     *disorder_out = P.disorder;
     *fallback_needed = P.npieces == 0;
     return 0;
