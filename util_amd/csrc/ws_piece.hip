@@ -553,15 +553,13 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     return 0;
 }
 
-// "piece_lds": bytes of unused dynamic LDS per K2 block, which caps its
-// blocks (= waves per SIMD) per CU. 0 (default): the CU's LDS / 7 when the batch holds at
-// least one segment per 8 pieces, else / 6. K2 needs only 60 VGPRs (8 waves/SIMD would fit);
-// with nontemporal stores it streamed best at 6 blocks per CU (round 3: cfg2 K1 + K2 1.355 ms
-// at 6 against 1.375-1.378 at 4 and 5, 1.374 at 7, profiles/r03_k2_occupancy.log); with the
-// sc1|nt stores (round 4) batches dense in segments (cfg2: 1 per 4 pieces, a wave's item and
-// segment lookups take longer) gain a seventh block (cfg2 -0.45-0.7 % on two boxes), while
-// large-frame batches (cfg3 1 per 44 pieces, cfg4 1 per 64) keep 6 (+0.6-0.75 % at 7;
-// profiles/r04_k2_occupancy_sc1.log). gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
+// "piece_lds": bytes of unused dynamic LDS per K2 block, which caps its blocks (= waves per
+// SIMD) per CU. 0 (default): the CU's LDS / 7 for frames of <= 16 KiB, else / 6 (ws_piece_dyn_lds).
+// K2 needs only 60 VGPRs (8 waves/SIMD would fit); with nontemporal stores it streamed best at 6
+// (round 3, profiles/r03_k2_occupancy.log); with the sc1|nt stores (round 4) pieces holding
+// several frames gain a seventh block (cfg2 -0.5-1.4 %, cfg2 in 64-frame segments -1.8 %), large
+// frames keep 6 (cfg3 +0.6 %, cfg4 +0.75 % at 7), 8 loses 2 % (profiles/r04_k2_occupancy_sc1.log).
+// gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
                           // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
