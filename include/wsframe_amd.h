@@ -212,15 +212,18 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * configuration; every value yields bit-identical results, each one is parity-tested in
  * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "scan_alpha"
  * (the piece path's segment walk: 1 switches to alphabet speculation over the lengths seen so far
- * once lengths keep changing, 0 stride speculation only), "piece_lds"
+ * once lengths keep changing, 0 stride speculation only), "piece_keys" (1: the frames of a segment's
+ * uniform prefix — masked, one wire and header length — get a 4-byte key in the workspace and the
+ * unmask derives their ranges from the segment, 0: a 16-byte item per frame), "piece_lds"
  * (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 7 when the previous call on the stream advised
  * frames of one length <= 16 KiB, / 6 for longer ones, and without advice / 7 for batches with
  * at least one segment per 8 pieces of 16 KiB, else / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
- * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
- * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
+ * fused kernel's window/occupancy), "enc_front" (encode: 1 single-pass look-back front with the
+ * edge chunks before the copy, 2 the same front as three launches, 0 hipcub scan and an edge
+ * kernel after it), "host_chunk_mb",
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:
  * chunk-parallel walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront;
  * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
@@ -234,7 +237,8 @@ WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long va
  * (chunks of a long stream written from the chunk-parallel walk's records),
  * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront), "stream_skips" (eager raw-stream
  * calls since load that skipped the pass rounds because the previous chunk walk on the stream saw
- * lengths that keep changing); with the option
+ * lengths that keep changing), "capture_adoptions" (graph captures since load that took over the
+ * workspace slot of a destroyed graph whose replays had all finished); with the option
  * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece
  * path's unmask launches since the option was set, from HIP events around each launch;
  * reading them waits for those launches). Returns 0, or -1 for an unknown name. */

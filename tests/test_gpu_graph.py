@@ -337,6 +337,65 @@ def test_capture_only_process_reuses_dead_slots(dev, kind):
     assert W.get_stat("workspace_bytes") <= base, (base, W.get_stat("workspace_bytes"))
 
 
+def test_capture_does_not_adopt_a_slot_whose_replay_is_queued(dev):
+    """a graph destroyed while its replay is still queued (behind a spinning kernel)
+    must not hand its workspace to a new capture — the new capture's slot re-zeroing would race
+    the pending replay. The capture made while the replay waits adopts nothing; one made after it
+    finished adopts the dead slot; every replay is bit-exact vs the oracle."""
+    import gc
+    import time
+    rng = np.random.default_rng(45)
+    wire, so, sl = random_stream(rng, 200)
+    n = len(wire)
+    ob = wire.copy()
+    oracle_segments(ob, so, sl, 16)
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    so_t = torch.tensor(so, dtype=torch.int64, device=dev)
+    sl_t = torch.tensor(sl, dtype=torch.int64, device=dev)
+    desc = torch.zeros(len(so) * 16 * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(len(so) * 16, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(wire).to(dev)
+
+    def capture(stream):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(stream):
+            g.capture_begin()
+            W.batch_decode_device(d, so_t, sl_t, 16, desc, res)
+            g.capture_end()
+        return g
+
+    W.batch_decode_device(d, so_t, sl_t, 16, desc, res)   # eager: frees earlier tests' dead slots
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    g1 = capture(side)
+    d[:n].copy_(src)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(400_000_000)               # ~0.2 s of spinning ahead of the replay
+    g1.replay()
+    del g1
+    for _ in range(3):
+        gc.collect()
+    a0 = W.get_stat("capture_adoptions")
+    g2 = capture(side)                           # the replay is still queued behind the spin
+    assert W.get_stat("capture_adoptions") == a0
+    torch.cuda.synchronize()
+    assert np.array_equal(d[:n].cpu().numpy(), ob)
+    d[:n].copy_(src)
+    g2.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(d[:n].cpu().numpy(), ob)
+    del g2
+    for _ in range(3):
+        gc.collect()
+        time.sleep(0.01)
+    g3 = capture(side)                           # every replay done: a dead slot is adopted
+    assert W.get_stat("capture_adoptions") == a0 + 1
+    d[:n].copy_(src)
+    g3.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(d[:n].cpu().numpy(), ob)
+
+
 @pytest.mark.parametrize("path", [1, 2], ids=["fused", "three_kernel"])
 def test_reassemble_graph_replay(dev, path):
     """websocketframeBatchReassembleDeviceEx captured in a graph (fused kernel, or scan +

@@ -214,6 +214,79 @@ def test_long_stream_endings(dev, cut):
     run(dev, wire, max_frames)
 
 
+def _cut_stream(cut, rng, wire, keep_len=False):
+    """the stream `wire` ended inside the parallel walk by `cut` (max_frames is the caller's);
+    keep_len: the same length (a captured call's length is fixed)"""
+    if cut == "truncated" and not keep_len:
+        return wire[:len(wire) - 1000].copy()
+    w = wire.copy()
+    if cut == "garbage":
+        at = 20 << 20
+        if keep_len:
+            w[at:at + 37] = rng.integers(0, 256, 37, dtype=np.uint8)
+        else:
+            w = np.concatenate([wire[:at], rng.integers(0, 256, 37, dtype=np.uint8), wire[at:]])
+    elif cut == "wrap":
+        # a masked 64-bit length that wraps the u64 sum (LEN_WRAP) at the first frame start after 25 MiB
+        od, orr = oracle_segments(wire.copy(), [0], [len(wire)], 1 << 16)
+        fo = od["frame_off"][:int(orr[0]["n_frames"])]
+        at = int(fo[np.searchsorted(fo, 25 << 20)])
+        bad = np.frombuffer(bytes([0x82, 0xFF]) + (0xFFFFFFFFFFFFFFF0).to_bytes(8, "big") + bytes(4), dtype=np.uint8)
+        if keep_len:
+            w[at:at + len(bad)] = bad
+        else:
+            w = np.concatenate([wire[:at], bad, wire[at:]])
+    return w
+
+
+@pytest.mark.parametrize("cut", ["max_frames", "truncated", "garbage", "wrap"])
+def test_skip_path_stream_endings(dev, cut):
+    """the eager skip path (no pass rounds: the plan kernel starts the walk at 0 and
+    does the first round's chores) on purpose, not by test order — a mixed-length call sets the
+    walk hint, then the cut stream is decoded: the call must skip the rounds and be bit-exact"""
+    rng = np.random.default_rng(81)
+    wire = long_stream(rng, 32 << 20, mix3)
+    W.set_option("stream_rw", 1)
+    run(dev, wire, 1 << 16)                                   # sets the hint (or keeps it set)
+    n0 = W.get_stat("stream_skips")
+    run(dev, wire, 1 << 16)
+    assert W.get_stat("stream_skips") == n0 + 1               # the hint is set now
+    cw = _cut_stream(cut, rng, wire)
+    n0 = W.get_stat("stream_skips")
+    run(dev, cw, 1200 if cut == "max_frames" else 1 << 16)
+    assert W.get_stat("stream_skips") == n0 + 1, cut
+
+
+@pytest.mark.parametrize("cut", ["max_frames", "garbage", "wrap"])
+def test_skip_path_stream_endings_captured(dev, cut):
+    """the same cuts in a captured raw-stream decode: replays of mixed bytes set the device hint,
+    so the replay of the cut bytes skips its rounds on the device; every replay bit-exact"""
+    rng = np.random.default_rng(82)
+    wire = long_stream(rng, 32 << 20, mix3)
+    cw = _cut_stream(cut, rng, wire, keep_len=True)
+    n = len(wire)
+    mf = 1200 if cut == "max_frames" else 1 << 16
+    d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(mf * 32, dtype=torch.uint8, device=dev)
+    res = torch.zeros(16, dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        W.stream_decode_device(d, n, mf, desc, res)
+    for w in (wire, wire, cw, wire, cw):
+        ob = w.copy()
+        od, orr = oracle_segments(ob, [0], [n], mf)
+        d[:n].copy_(torch.from_numpy(w).to(dev))
+        desc.zero_()
+        res.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+        assert tuple(gr) == tuple(orr[0]), (cut, gr, orr[0])
+        assert np.array_equal(desc.cpu().numpy().view(W.DESC_DTYPE)[:int(gr["n_frames"])],
+                              od[:int(orr[0]["n_frames"])])
+        assert np.array_equal(d[:n].cpu().numpy(), ob)
+
+
 def test_long_stream_same_as_serial(dev, serial_walk):
     """the one-wavefront walk on a chunk-parallel-sized stream (the option's other side)"""
     wire = long_stream(np.random.default_rng(28), 17 << 20, mix3)

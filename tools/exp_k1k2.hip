@@ -16,7 +16,13 @@
 //   11 latency-bound chase kernel (arg % 1000 x 10 us; 256 blocks if arg > 1000, else 1) + K2   12 it alone
 //   20-23 a pass of arg MiB over another buffer + K2 (20 nt XOR, 21 plain write-only, 22 nt
 //   write-only, 23 plain read-only); 30-33 the same pass alone
+//   40 K1 variant `arg` alone, 41 it + K2 (round 5 breakdown; the library must be built with
+//   tools/exp_k1k2.sh, which compiles ws_piece.hip with WS_K1_VARIANTS): arg = store bitmask
+//   (1 descriptors, 2 items, 4 piece pointers, 8 segment records; 16 = all stores at 8 waves/SIMD),
+//   first step guessing the stride `stride` (the product's hinted call)
 #include "../util_amd/csrc/ws_common.h"
+int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, u32 g0, int st,
+                                 PieceWs* out);
 
 __global__ void exp_spin_kernel(unsigned long long ticks) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -182,6 +188,9 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
             if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P))) return rc;
             break;
         case 9: case 10: if ((rc = ws_launch_piece_scan(L, 0, buflen, ws, gen, &P, false, (u32)arg))) return rc; break;
+        case 40: case 41:
+            if ((rc = ws_launch_piece_scan_variant(L, 0, buflen, ws, gen, (u32)stride, (int)arg, &P))) return rc;
+            break;
         case 20: case 30: case 21: case 31: case 22: case 32: case 23: case 33: {   // pass of arg MiB (+ K2 for 2x)
             gu32x4* o = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(other));
             const unsigned long long n16 = (unsigned long long)arg << 16;
@@ -194,7 +203,7 @@ extern "C" __attribute__((visibility("default"))) int exp_k1k2_run(
         }
         default: break;
         }
-        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16) || mode == 18 || (mode >= 20 && mode <= 23)) &&
+        if ((mode <= 5 || mode == 9 || mode == 11 || (mode >= 13 && mode <= 16) || mode == 18 || (mode >= 20 && mode <= 23) || mode == 41) &&
             (rc = ws_launch_piece_unmask(L, P, gen)))
             return rc;
     }

@@ -19,6 +19,9 @@ wl = bench.Workload.make(os.environ.get("EXP_CFG", "cfg2"), dev)
 lib = C.CDLL(os.path.join(here, os.environ.get("EXP_LIB", "libexp_k1k2.so")))
 lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
 ldsv = [int(x) for x in os.environ.get("EXP_LDS", "0").split(",")]
+for kv in filter(None, os.environ.get("EXP_OPTS", "").split(",")):    # e.g. EXP_OPTS=piece_keys=0
+    k, _, v = kv.partition("=")
+    assert lib.websocketframeGpuSetOption(k.encode(), int(v)) == 0, kv
 f = lib.exp_k1k2_run
 f.restype = C.c_int
 vp, u64 = C.c_void_p, C.c_ulonglong
@@ -29,7 +32,7 @@ nframes = wl.nframes
 stride = int(os.environ.get("EXP_STRIDE", "4104"))
 names = {0: "K1+K2", 1: "K2", 2: "spin40+K2", 3: "hdrtouch+K2", 4: "midtouch+K2", 5: "othertouch+K2",
          6: "hdrtouch", 7: "K1", 8: "spin40", 9: "K1g+K2", 10: "K1g", 11: "chase+K2", 12: "chase", 13: "K1+xor+K2", 14: "wsread+K2", 15: "K1K1+K2", 16: "alu+K2", 17: "alu", 18: "xor+K2", 19: "xor",
-         20: "ntxor+K2", 21: "wr+K2", 22: "ntwr+K2", 23: "rd+K2", 30: "ntxor", 31: "wr", 32: "ntwr", 33: "rd"}
+         20: "ntxor+K2", 21: "wr+K2", 22: "ntwr+K2", 23: "rd+K2", 30: "ntxor", 31: "wr", 32: "ntwr", 33: "rd", 40: "K1v", 41: "K1v+K2"}
 seq = [(0, 0), (1, 0), (2, 40), (3, 0), (4, 2048), (5, 0), (6, 0), (7, 0), (8, 40), (2, 10)]
 if os.environ.get("EXP_MODES"):
     seq = [tuple(int(y) for y in x.split(":")) for x in os.environ["EXP_MODES"].split(",")]

@@ -31,10 +31,12 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
+extern WsOpt ws_piece_keys;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips;
+extern std::atomic<unsigned long long> ws_stat_adoptions;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -85,7 +87,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_reasm_cfg = (int)value;
     }
     else if (!strcmp(name, "enc_front")) {
-        if (value < 0 || value > 1) return -1;
+        if (value < 0 || value > 2) return -1;
         ws_enc_front = (int)value;
     }
     else if (!strcmp(name, "stream_rw")) {
@@ -108,6 +110,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 0 || value > 1) return -1;
         ws_scan_alpha = (int)value;
     }
+    else if (!strcmp(name, "piece_keys")) {
+        if (value < 0 || value > 1) return -1;
+        ws_piece_keys = (int)value;
+    }
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = value ? 1 : 0;
         ws_k2_timing_reset();
@@ -128,6 +134,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
     else if (!strcmp(name, "stream_skips")) *value = ws_stat_stream_skips.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
+    else if (!strcmp(name, "capture_adoptions")) *value = ws_stat_adoptions.load();
 
     else return -1;
     return 0;
@@ -155,6 +162,8 @@ struct WsStreamWs {
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
+    void* lws = nullptr;           // look-back scan state (zero at allocation; every call leaves it zero)
+    size_t lws_bytes = 0;
     void* aws = nullptr;           // auxiliary device scratch (the stream path's chunk-parallel walk)
     size_t aws_bytes = 0;
     void* hws = nullptr;           // ... and its pinned host copy
@@ -163,7 +172,9 @@ struct WsStreamWs {
     bool aux_state_ok = false;     // the stream path's state (aux head) rests at zero
     int* adv_h = nullptr;          // pinned host words: the device's stride hint for the next call
     int* adv_d = nullptr;
-    std::vector<void*> retired;    // buffers replaced while capturing (the graph still uses them)
+    std::vector<std::pair<void*, size_t>> retired;   // buffers replaced while capturing (the graph still uses them)
+    hipEvent_t done = nullptr;     // captured slots: recorded at the end of every captured call (an event
+                                   // record node), so a destroyed graph's replays are known to be finished
 };
 struct WsDevState {
     int init = 0;
@@ -171,14 +182,20 @@ struct WsDevState {
     int lds = 0;
     std::deque<WsStreamWs> sw;     // grows; stable addresses
     unsigned long long tick = 0;
+    std::vector<std::pair<void*, size_t>> deferred;   // adopted slots' retired buffers: freed by the next eager call
 };
 static WsDevState g_dev[WS_MAX_DEV];
 static std::mutex g_dev_mu;        // device init and the stream-slot table
 size_t ws_workspace_bytes_total() {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     size_t t = 0;
-    for (auto& d : g_dev)
-        for (auto& w : d.sw) t += w.ws_bytes + w.ews_bytes + w.aws_bytes;
+    for (auto& d : g_dev) {
+        for (auto& w : d.sw) {
+            t += w.ws_bytes + w.ews_bytes + w.aws_bytes + w.lws_bytes;
+            for (auto& r : w.retired) t += r.second;
+        }
+        for (auto& r : d.deferred) t += r.second;
+    }
     return t;
 }
 
@@ -218,14 +235,15 @@ static bool capturing(hipStream_t stream) {
 static void slot_free(WsStreamWs& w) {
     (void)hipFree(w.ws);
     (void)hipFree(w.ews);
+    (void)hipFree(w.lws);
     (void)hipFree(w.aws);
     if (w.hws) (void)hipHostFree(w.hws);
     if (w.adv_h) (void)hipHostFree(w.adv_h);
-    for (void* p : w.retired) (void)hipFree(p);
+    for (auto& r : w.retired) (void)hipFree(r.first);
     w.retired.clear();
-    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
+    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr; w.lws = nullptr;
     w.adv_h = nullptr; w.adv_d = nullptr;
-    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = 0;
+    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = w.lws_bytes = 0;
     w.aux_state_ok = false;
     w.stream = nullptr;
     w.capture = 0;
@@ -234,7 +252,20 @@ static void slot_free(WsStreamWs& w) {
     w.dead = 0;
 }
 
+std::atomic<unsigned long long> ws_stat_adoptions{0};
 static void capture_slot_destroyed(void* p) { reinterpret_cast<WsStreamWs*>(p)->dead.store(1); }
+
+// a destroyed graph's slot may be adopted only once every replay that was launched has finished:
+// its calls end with an event record node, so the event is complete (or was never recorded) then.
+// The user object's release alone does not say that (hipUserObjectNoDestructorSync).
+static bool replays_done(WsStreamWs& w) {
+    if (!w.done) return true;
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+    const hipError_t e = hipEventQuery(w.done);
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+    return e == hipSuccess;
+}
 
 // zero the resting heads of a slot's buffers (decode/reassembly/stream workspace: 16 B; the
 // auxiliary scratch: WS_AUX_HEAD) outside any capture: private stream, relaxed capture mode
@@ -245,7 +276,7 @@ static int slot_rezero(WsStreamWs& w) {
     hipStream_t ps = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
     if (e == hipSuccess && w.ws) e = hipMemsetAsync(w.ws, 0, 16, ps);
-    if (e == hipSuccess && w.aws) e = hipMemsetAsync(w.aws, 0, WS_AUX_HEAD, ps);
+    if (e == hipSuccess && w.aws) e = hipMemsetAsync(w.aws, 0, w.aws_bytes < WS_AUX_ZERO ? w.aws_bytes : WS_AUX_ZERO, ps);
     if (e == hipSuccess) e = hipStreamSynchronize(ps);
     if (ps) (void)hipStreamDestroy(ps);
     (void)hipThreadExchangeStreamCaptureMode(&m);
@@ -276,6 +307,8 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
         (void)hipThreadExchangeStreamCaptureMode(&mode);
         for (WsStreamWs& w : ds->sw)
             if (w.used && w.captured && w.dead.load() && !w.busy) slot_free(w);
+        for (auto& r : ds->deferred) (void)hipFree(r.first);
+        ds->deferred.clear();
         (void)hipThreadExchangeStreamCaptureMode(&mode);
     }
     WsStreamWs* lru = nullptr;
@@ -294,7 +327,7 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
             continue;
         }
         if (w.captured && w.dead.load() && !w.busy) {
-            if (!adopt) adopt = &w;
+            if (!adopt && cap && replays_done(w)) adopt = &w;
             continue;
         }
         if (!w.captured) {
@@ -311,6 +344,10 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
         if (rc) return rc;
         w = adopt;
         w->dead = 0;
+        ++ws_stat_adoptions;
+        // the buffers its dead graph's capture replaced: free at the next eager call (not inside a capture)
+        ds->deferred.insert(ds->deferred.end(), w->retired.begin(), w->retired.end());
+        w->retired.clear();
     } else if (freeslot) {
         w = freeslot;
     } else if (cap || eager < WS_STREAM_SLOTS || !lru) {
@@ -330,7 +367,8 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
     if (cap && graph) {
         // tie the slot's lifetime to the graph being captured
         hipUserObject_t uo = nullptr;
-        hipError_t e = hipUserObjectCreate(&uo, w, capture_slot_destroyed, 1, hipUserObjectNoDestructorSync);
+        hipError_t e = w->done ? hipSuccess : hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipUserObjectCreate(&uo, w, capture_slot_destroyed, 1, hipUserObjectNoDestructorSync);
         if (e == hipSuccess) e = hipGraphRetainUserObject(graph, uo, 1, hipGraphUserObjectMove);
         if (e != hipSuccess) {
             // the slot is not tied to any graph: hand it back (its buffers stay for the next user)
@@ -356,7 +394,7 @@ static int grow(WsStreamWs* w, void** p, size_t* have, size_t bytes, hipStream_t
     const bool cap = capturing(stream);
     if (*p) {
         if (cap) {
-            w->retired.push_back(*p);
+            w->retired.emplace_back(*p, *have);
         } else {
             if ((e = hipStreamSynchronize(stream)) != hipSuccess) return ws_set_err("hipStreamSynchronize", e);
             (void)hipFree(*p);
@@ -393,6 +431,8 @@ WsSlot::~WsSlot() { release(); }
 
 void WsSlot::release() {
     if (!w) return;
+    // a captured call ends with an event record node (replays_done)
+    if (w->captured && w->done && capturing(st)) (void)hipEventRecord(w->done, st);
     std::lock_guard<std::mutex> lk(g_dev_mu);
     --w->busy;
     w = nullptr;
@@ -420,6 +460,16 @@ int WsSlot::workspace(size_t bytes, size_t zero_bytes, void** out) {
     return 0;
 }
 
+// single-pass look-back scan state (ws_encode.hip): zeroed whole at every (re)allocation; each
+// call's last workgroup returns the words it used to zero, so the state rests at zero
+int WsSlot::lookback_state(size_t bytes, void** out) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    const int rc = grow(w, &w->lws, &w->lws_bytes, bytes, st, ~(size_t)0, "hipMalloc(look-back state)");
+    if (rc) return rc;
+    *out = w->lws;
+    return 0;
+}
+
 int WsSlot::encode_workspace(size_t bytes, void** out) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     const int rc = grow(w, &w->ews, &w->ews_bytes, bytes, st, 0, "hipMalloc(encode workspace)");
@@ -435,7 +485,7 @@ int WsSlot::aux(size_t dbytes, size_t hbytes, WsAux* out) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     const void* before = w->aws;
     const size_t have = w->aws_bytes;
-    int rc = grow(w, &w->aws, &w->aws_bytes, dbytes < WS_AUX_HEAD ? WS_AUX_HEAD : dbytes, st, WS_AUX_HEAD,
+    int rc = grow(w, &w->aws, &w->aws_bytes, dbytes < WS_AUX_HEAD ? WS_AUX_HEAD : dbytes, st, WS_AUX_ZERO,
                   "hipMalloc(aux workspace)");
     if (rc) return rc;
     if (w->aws != before || w->aws_bytes != have) w->aux_state_ok = true;   // freshly zeroed
