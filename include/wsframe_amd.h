@@ -212,9 +212,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * configuration; every value yields bit-identical results, each one is parity-tested in
  * tests/test_gpu_options.py): "path" (-1 auto, 1 walker, 3 piece, 4 segfuse), "scan_alpha"
  * (the piece path's segment walk: 1 switches to alphabet speculation over the lengths seen so far
- * once lengths keep changing, 0 stride speculation only), "piece_keys" (1: the frames of a segment's
- * uniform prefix — masked, one wire and header length — get a 4-byte key in the workspace and the
- * unmask derives their ranges from the segment, 0: a 16-byte item per frame), "piece_lds"
+ * once lengths keep changing, 0 stride speculation only), "piece_lds"
  * (unused dynamic LDS per unmask block:
  * caps its blocks per CU; 0 = the CU's LDS / 7 when the previous call on the stream advised
  * frames of one length <= 16 KiB, / 6 for longer ones, and without advice / 7 for batches with

@@ -19,7 +19,7 @@ wl = bench.Workload.make(os.environ.get("EXP_CFG", "cfg2"), dev)
 lib = C.CDLL(os.path.join(here, os.environ.get("EXP_LIB", "libexp_k1k2.so")))
 lib.websocketframeGpuSetOption.argtypes = [C.c_char_p, C.c_longlong]
 ldsv = [int(x) for x in os.environ.get("EXP_LDS", "0").split(",")]
-for kv in filter(None, os.environ.get("EXP_OPTS", "").split(",")):    # e.g. EXP_OPTS=piece_keys=0
+for kv in filter(None, os.environ.get("EXP_OPTS", "").split(",")):    # e.g. EXP_OPTS=scan_alpha=0
     k, _, v = kv.partition("=")
     assert lib.websocketframeGpuSetOption(k.encode(), int(v)) == 0, kv
 f = lib.exp_k1k2_run

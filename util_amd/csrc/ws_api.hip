@@ -31,7 +31,6 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
-extern WsOpt ws_piece_keys;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
@@ -109,10 +108,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "scan_alpha")) {
         if (value < 0 || value > 1) return -1;
         ws_scan_alpha = (int)value;
-    }
-    else if (!strcmp(name, "piece_keys")) {
-        if (value < 0 || value > 1) return -1;
-        ws_piece_keys = (int)value;
     }
     else if (!strcmp(name, "k2_timing")) {
         ws_k2_timing = value ? 1 : 0;

@@ -386,21 +386,18 @@ int ws_launch_walker(const WsLaunch& L, const u32* gate = nullptr, u32 gate_gen 
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 struct WsSegRec {         // K1 -> K2: one rx segment, origin-relative [lo, hi) (< 2^48, as the items)
     u64 w0, w1;           // and its item count: w0 = lo | cnt[15:0] << 48, w1 = hi | cnt[31:16] << 48
-    u64 w2, w3;           // its uniform prefix: w2 = u | L << 32, w3 = H — frames 0..u-1 are masked, of
-};                        // wire length L and header length H each (a 4-B key per frame, no item);
-                          // one 32-B scalar load in K2 instead of several dependent ones
+};                        // (one 16-B scalar load in K2 instead of three dependent ones)
 struct PieceWs {          // ws_piece.hip workspace views after K1
     u32* disorder;
     u32* nonuni;          // K1's count of segments with frames of several lengths (K2 reads + clears)
     u64* ptr;
     u32* nwork;           // items per segment (frames walked, incl. an unconsumed ret==0 frame)
     u32x4* items;         // per descriptor slot s*max_frames+k: P0|rk_lo<<48, P1|rk_hi<<48 (origin-relative)
-    u32* keys = nullptr;  // per descriptor slot: the pre-rotated key of a frame in its segment's uniform prefix
     WsSegRec* segr = nullptr;   // per segment (K1 writes it; the raw-stream path leaves it null)
     u64 npieces, pbase, c_lo, c_hi;
 };
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
-                         bool count_nonuniform = false, u32 g0 = 0, bool uniform_keys = false);
+                         bool count_nonuniform = false, u32 g0 = 0);
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice = nullptr, u32 g0 = 0);
 int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0 = 0);
 u32 ws_next_gen();

@@ -557,23 +557,33 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front1_kernel(const unsigned 
     const u64 incl = enc_wave_incl(wl, lane);
     if (lane == 63) ws[wv] = incl;
     __syncthreads();
-    if (tid == 0) {
+    if (wv == 0) {
+        // the look-back, by the first wavefront: 64 tiles per step (lane l reads tile t-1-l-64k),
+        // summing aggregates back to the nearest tile that has published its inclusive prefix
         const u64 tsum = ws[0] + ws[1] + ws[2] + ws[3];
+        if (lane == 0)
+            __hip_atomic_store(lb + t, (t == 0 ? LB_INC : LB_AGG) | tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         u64 pre = 0;
-        if (t == 0) {
-            __hip_atomic_store(lb, LB_INC | tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(lb + t, LB_AGG | tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (u32 j = t - 1;; --j) {                                      // tile j took its ticket before us
-                u64 w;
+        for (long long base = (long long)t - 1; base >= 0; base -= 64) {
+            const long long j = base - (long long)lane;
+            u64 w = LB_INC;                                                  // before tile 0: prefix 0
+            if (j >= 0) {
+                // every tile before us took its ticket earlier: it is running or done
                 while (!((w = __hip_atomic_load(lb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62))
                     __builtin_amdgcn_s_sleep(1);
-                pre += w & LB_VAL;
-                if ((w >> 62) == 2 || j == 0) break;
             }
-            __hip_atomic_store(lb + t, LB_INC | (pre + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64 incm = __ballot((w >> 62) == 2);
+            const u32 stop = incm ? (u32)__builtin_ctzll(incm) : 64u;     // the nearest inclusive prefix
+            u64 v = lane <= stop ? (w & LB_VAL) : 0;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor((unsigned long long)v, d, 64);
+            pre += v;
+            if (incm) break;
         }
-        s_pre = pre;
+        if (lane == 0) {
+            if (t) __hip_atomic_store(lb + t, LB_INC | (pre + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_pre = pre;
+        }
     }
     __syncthreads();
     u64 off = s_pre + incl - wl;

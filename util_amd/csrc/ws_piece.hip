@@ -77,8 +77,6 @@ struct WalkArgs {
     u64 pbase, lo, hi;
     u32 g0;
     u32 alpha_ok;         // option "scan_alpha": alphabet speculation allowed
-    u32* keys;            // uniform-prefix keys (per descriptor slot)
-    u32 ukeys;            // 1: frames of a segment's uniform prefix get a key instead of an item
 };
 
 // G = 16 lanes per segment, header walk by STRIDE SPECULATION: lane k of the group parses the
@@ -119,11 +117,6 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
     int status = WEBSOCKET_SEG_OK;
     bool nonu = false;                       // frames of another length than the first, or an error stop
     const u64 gmask = (1ull << G) - 1;
-    // UNIFORM PREFIX (round 5): frames 0..upre-1 of the segment that are masked, of the first frame's
-    // wire length R0 and header length H0, with no (int) truncation, need no item: K2 derives their
-    // payload range from the segment record (frame j at sorg + j*R0), so they get a 4-B key each
-    bool uopen = A.ukeys != 0;
-    u32 upre = 0, R0 = 0, H0 = 0;
     // ALPHABET SPECULATION (lengths that keep changing, e.g. cfg3): once a step ends after one
     // frame of a new length, the lanes speculate over the lengths seen so far (L0..L2, na of them)
     // instead of one stride: lane 0 parses the frame at off, lanes 1..na the frame after it for
@@ -221,30 +214,15 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
         const int ret_m = __shfl(h.ret, (int)(gb + lm));
         const int st_m = __shfl(st, (int)(gb + lm));
         const u32 ntake = active ? mm + ((code_m == 1 || code_m == 2) ? 1u : 0u) : 0u;
-        // the uniform prefix (stride lanes are in frame order; alphabet mode starts only after a
-        // length change, so the prefix has ended by then)
-        const u32 r0l = (u32)__shfl(h.ret, (int)gb), h0l = (u32)__shfl((int)h.hdr, (int)gb);
-        if (nf == 0) { R0 = r0l; H0 = h0l; }                                 // frame 0 (lane 0 of round 1)
-        const bool uok = h.ret > 0 && h.masked && (u64)(u32)h.ret == (u64)h.hdr + h.plen && (u32)h.ret == R0 &&
-                         h.hdr == H0;
-        const u64 ubad = (__ballot(!uok) >> gb) & gmask;
-        const u32 ub = alpha ? 0u : (ubad ? (u32)__builtin_ctzll(ubad) : G);
-        const bool upfx = uopen && gl < ub;                                  // (if mine) a prefix frame
-        if (uopen) {
-            upre = nf + (ub < ntake ? ub : ntake);
-            uopen = ub >= ntake;
-        }
         // this lane's frame is consumed: its index in the segment is nf + depth
         const bool mine = alpha ? depth < ntake && gl == (depth == 0 ? 0u : (depth == 1 ? cl1 : (depth == 2 ? cl2 : cl3)))
                                 : gl < ntake;
         const u64 fo = sorg + pos;
         const u64 p0 = fo + h.hdr, fe = p0 + h.plen;
         if (mine) {                                                         // consumed frames, in parallel
-            if (ST & 2) {
-                const u32 rk = rotl32(h.key, 8u * (u32)(p0 & 3));
-                if (upfx) *gptr<u32>(A.keys + ibase + nf + depth) = rk;
-                else put_item(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0, rk);
-            }
+            if (ST & 2)
+                put_item(gptr<u32x4>(A.items + ibase + nf + depth), p0, h.masked ? fe : p0,
+                         rotl32(h.key, 8u * (u32)(p0 & 3)));
             if ((ST & 1) && h.ret != 0) ws_store_desc(A.desc + dbase + nf + depth, so + pos, h);
         }
         // the pieces whose first byte lies in a consumed frame point at it: a lane writes its frame's
@@ -327,9 +305,6 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
             ws_store_res(A.res + sc, off, nf, status);
             *gptr<u32>(A.nwork + sc) = cnt;
             put_item(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)), sorg, sorg + sl, cnt);   // WsSegRec
-            u32x4 r2;
-            r2.x = upre; r2.y = R0; r2.z = H0; r2.w = 0;
-            *(gptr<u32x4>(reinterpret_cast<u32x4*>(A.segr + sc)) + 1) = r2;
             cnt_out = cnt;
             nonu_out = nonu;
         }
@@ -369,8 +344,7 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
                                                                   WebsocketFrameDesc_t* __restrict__ desc,
                                                                   WebsocketSegResult_t* __restrict__ res,
                                                                   u32 wshift, u64 ppw, u64 npieces, u32* nonuni,
-                                                                  int* advice, const WsSegRec* __restrict__ segr,
-                                                                  const u32* __restrict__ keys) {
+                                                                  int* advice, const WsSegRec* __restrict__ segr) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     // block -> piece: the pieces form 2^wshift windows of ppw pieces streamed side by side
@@ -425,15 +399,13 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     while (s < nseg) {
         // the segment: SR = K1's 32-B record (one scalar load), else the caller's tables
         u64 slo, shi;
-        u32 cnt, upre = 0, R0 = 0, H0 = 0;
+        u32 cnt;
         if (SR) {
-            const auto* rp = reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(
+            const u32x4 R = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(
                 reinterpret_cast<uintptr_t>(segr + s));
-            const u32x4 R = rp[0], R2 = rp[1];
             const u64 w0 = (u64)R.x | ((u64)R.y << 32), w1 = (u64)R.z | ((u64)R.w << 32);
             slo = w0 & 0xFFFFFFFFFFFFull; shi = w1 & 0xFFFFFFFFFFFFull;
             cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
-            upre = R2.x; R0 = R2.y; H0 = R2.z;                              // the uniform prefix
         } else {
             slo = seg_off[s] + lead0; shi = slo + seg_len[s]; cnt = nwork[s];
         }
@@ -457,20 +429,11 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             // after that — all 64 lanes loading would fetch 1 KiB of items per wave in long segments
             const u32 j = k + lane;
             const bool valid = j < cnt && lane < step;
-            u64 P0 = 0, P1 = 0;
-            u32 rk = 0;
-            if (valid && j < upre) {                                        // uniform prefix: range from the record
-                rk = keys[(u64)s * max_frames + j];
-                const u64 fo = slo + (u64)j * R0;
-                P0 = fo + H0;
-                P1 = fo + R0;
-            } else if (valid) {
-                const u32x4 q = items[(u64)s * max_frames + j];
-                const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
-                P0 = w0 & 0xFFFFFFFFFFFFull;
-                P1 = w1 & 0xFFFFFFFFFFFFull;
-                rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
-            }
+            u32x4 q = {0, 0, 0, 0};
+            if (valid) q = items[(u64)s * max_frames + j];
+            const u64 w0 = (u64)q.x | ((u64)q.y << 32), w1 = (u64)q.z | ((u64)q.w << 32);
+            const u64 P0 = w0 & 0xFFFFFFFFFFFFull, P1 = w1 & 0xFFFFFFFFFFFFull;
+            const u32 rk = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
             // items are in address order: the first one starting at/after r1 ends the scan
             const u64 past = __ballot(valid && P0 >= r1);
             const u32 nlim = past ? (u32)__builtin_ctzll(past) : 64u;
@@ -553,15 +516,12 @@ size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames) {
     size_t b = (16 + npieces * 8 + 15) & ~(size_t)15;
     b = (b + (size_t)nseg * 4 + 31) & ~(size_t)31;
     b += (size_t)nseg * sizeof(WsSegRec);
-    return b + (size_t)nseg * max_frames * (16 + 4) + 16;
+    return b + (size_t)nseg * max_frames * 16 + 16;
 }
 
 // "scan_alpha": 1 (default) the walk switches to alphabet speculation once lengths keep changing,
 // 0 stride speculation only (round 3's walk)
 WsOpt ws_scan_alpha{1};
-// "piece_keys": 1 (default) frames of a segment's uniform prefix get a 4-B key instead of a 16-B item
-// (the decode's K1 + K2; the reassembly's scan always writes items), 0 items for every frame
-WsOpt ws_piece_keys{1};
 
 // K1 alone (also the first stage of the reassembly path, ws_reasm.hip). Segments lie in
 // [lo, hi) of L.buf. count_nonuniform: K1 counts segments with frames of several lengths
@@ -582,23 +542,19 @@ static WalkArgs piece_scan_args(const WsLaunch& L, u64 lo, u64 hi, unsigned char
     P.segr = reinterpret_cast<WsSegRec*>(ws + b);
     b += (size_t)L.nseg * sizeof(WsSegRec);
     P.items = reinterpret_cast<u32x4*>(ws + b);
-    P.keys = reinterpret_cast<u32*>(ws + b + (size_t)L.nseg * L.max_frames * 16);
     WalkArgs W;
     W.buf = L.buf; W.seg_off = L.seg_off; W.seg_len = L.seg_len; W.nseg = L.nseg; W.max_frames = L.max_frames;
     W.desc_base = L.desc_base; W.desc = L.desc; W.res = L.res; W.items = P.items; W.ptr = P.ptr; W.nwork = P.nwork;
     W.segr = P.segr; W.disorder = P.disorder; W.gen = gen; W.pbase = P.pbase; W.lo = lo; W.hi = hi;
     W.g0 = g0 < (1u << 31) ? g0 : 0u;
     W.alpha_ok = ws_scan_alpha ? 1u : 0u;
-    W.keys = P.keys;
-    W.ukeys = 0;
     return W;
 }
 
 int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, PieceWs* out,
-                         bool count_nonuniform, u32 g0, bool uniform_keys) {
+                         bool count_nonuniform, u32 g0) {
     PieceWs P;
-    WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
-    W.ukeys = uniform_keys && ws_piece_keys ? 1u : 0u;
+    const WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
     const u32 blocks = (u32)(((u64)L.nseg * WALK_G + PSCAN_T - 1) / PSCAN_T);
     hipLaunchKernelGGL(ws_piece_scan_kernel<15>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, W,
                        count_nonuniform ? P.nonuni : nullptr);
@@ -623,8 +579,7 @@ __global__ __launch_bounds__(PSCAN_T) __attribute__((amdgpu_waves_per_eu(8, 8)))
 int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, u32 g0, int st,
                                  PieceWs* out) {
     PieceWs P;
-    WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
-    W.ukeys = ws_piece_keys ? 1u : 0u;
+    const WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
     const dim3 g((u32)(((u64)L.nseg * WALK_G + PSCAN_T - 1) / PSCAN_T)), b(PSCAN_T);
     switch (st) {
     case 0: hipLaunchKernelGGL(ws_piece_scan_kernel<0>, g, b, 0, L.stream, W, nullptr); break;
@@ -728,12 +683,12 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
         hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
-                           advice, (const WsSegRec*)P.segr, (const u32*)P.keys);
+                           advice, (const WsSegRec*)P.segr);
     else
         hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
                            P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
-                           advice, (const WsSegRec*)nullptr, (const u32*)nullptr);
+                           advice, (const WsSegRec*)nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
     return timing ? ws_k2_mark(L.stream, true, &tslot) : 0;
@@ -744,7 +699,7 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,
                     const u32** disorder_out, bool* fallback_needed, u32 g0) {
     PieceWs P;
-    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr, g0, true);
+    int rc = ws_launch_piece_scan(L, lo, hi, ws, gen, &P, advice != nullptr, g0);
     if (rc) return rc;
     if ((rc = ws_launch_piece_unmask(L, P, gen, advice, g0))) return rc;
     *disorder_out = P.disorder;
