@@ -743,7 +743,7 @@ def run_strong(args, dev, world, rank):
         "config": {"workload": "8M masked binary frames x 64 KiB, 16-frame rx segments, one batch sharded by segment "
                                "ranges", "config": args.config, "global_frames": n_total,
                    "global_wire_bytes": glob["wire"], "global_payload_bytes": glob["payload"],
-                   "rounds_per_rank": loc["rounds"], "frames_per_round": per_round * fps,
+                   "rounds_per_rank": loc["rounds"], "frames_per_round": per_round * fps, "alloc": args.alloc,
                    "parallelism": "segment-range shards over %d GPU(s), no data-path collective" % world},
         "roofline": {"bound": "hbm", "achieved": round(algo / world / step_s / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s per GPU", "frac": round(algo / world / step_s / 1e9 / PEAK_HBM_GBS, 4),
@@ -908,6 +908,10 @@ def main():
                     help="decode: also time K independent batches of the config in flight together, one HIP "
                          "stream each (a reactor with successive rx batches), reported as the 'inflight' field "
                          "(1 = off)")
+    ap.add_argument("--alloc", default="torch", choices=["torch", "contiguous"],
+                    help="device buffers from torch's caching allocator (default), or every allocation "
+                         "physically contiguous (libwsframe_amd_bench.so as torch's pluggable allocator; "
+                         "DESIGN §4: cfg4's slow mode on boxes whose memory earlier processes fragmented)")
     ap.add_argument("--op", default="decode", choices=["decode", "encode", "reasm", "stream"],
                     help="decode (the headline), client-side encode + mask of the same frames, fused "
                          "decode + message reassembly (use with --config cfg5), or the whole batch as ONE raw "
@@ -936,6 +940,10 @@ def main():
 
     import torch
     import torch.distributed as dist
+    if args.alloc == "contiguous":                                 # before any device allocation
+        from util_amd import _lib
+        torch.cuda.memory.change_current_allocator(torch.cuda.memory.CUDAPluggableAllocator(
+            _lib.BENCH_LIB_PATH, "websocketframeBenchTorchAlloc", "websocketframeBenchTorchFree"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

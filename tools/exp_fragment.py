@@ -16,8 +16,10 @@ while total < gib * 2**30:
     total += n
 held = held[::2]
 torch.cuda.empty_cache()
-more = []
-for _ in range(len(held) // 2):
-    more.append(torch.empty(random.choice([89, 144, 233]) << 20, dtype=torch.uint8, device="cuda"))
+more, extra = [], 0
+while extra < gib / 4 * 2**30:
+    n = random.choice([89, 144, 233]) << 20
+    more.append(torch.empty(n, dtype=torch.uint8, device="cuda"))
+    extra += n
 torch.cuda.synchronize()
 print("fragmenter: %d + %d allocations held, %.1f GiB reserved" % (len(held), len(more), torch.cuda.memory_reserved() / 2**30))

@@ -45,7 +45,9 @@ EXPORTS = REFERENCE_EXPORTS + [
 # include/wsframe_amd_bench.h (libwsframe_amd_bench.so)
 BENCH_EXPORTS = ["websocketframeSynthDevice", "websocketframeSynthVerifyDevice", "websocketframeGpuCalibrate",
                  "websocketframeBenchLastError", "websocketframeSynthDeviceRange",
-                 "websocketframeSynthVerifyDeviceRange", "websocketframeFrameHashDevice"]
+                 "websocketframeSynthVerifyDeviceRange", "websocketframeFrameHashDevice",
+                 "websocketframeBenchAlloc", "websocketframeBenchFree", "websocketframeBenchTorchAlloc",
+                 "websocketframeBenchTorchFree"]
 
 
 def build_lib(force=False):

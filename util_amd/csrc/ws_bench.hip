@@ -19,6 +19,34 @@ int ws_set_msg(const char* msg) {
 }
 extern "C" WSFRAME_AMD_EXPORT const char* websocketframeBenchLastError(void) { return g_bench_error; }
 
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBenchAlloc(void** d_ptr, unsigned long long nbytes, unsigned int flags) {
+    const hipError_t e = hipExtMallocWithFlags(d_ptr, nbytes, flags);
+    return e == hipSuccess ? 0 : ws_set_err("hipExtMallocWithFlags", e);
+}
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBenchFree(void* d_ptr) {
+    const hipError_t e = hipFree(d_ptr);
+    return e == hipSuccess ? 0 : ws_set_err("hipFree", e);
+}
+extern "C" WSFRAME_AMD_EXPORT void* websocketframeBenchTorchAlloc(long long nbytes, int device, void* hip_stream) {
+    (void)hip_stream;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocContiguous) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        if (hipMalloc(&p, (size_t)nbytes) != hipSuccess) p = nullptr;
+    }
+    if (cur != device) (void)hipSetDevice(cur);
+    return p;
+}
+extern "C" WSFRAME_AMD_EXPORT void websocketframeBenchTorchFree(void* d_ptr, long long nbytes, int device,
+                                                              void* hip_stream) {
+    (void)nbytes; (void)device; (void)hip_stream;
+    (void)hipFree(d_ptr);
+}
+
 // ---------------------------------------------------------------------------------------------
 // synthetic batches (bench/test input; ws_synth.h)
 

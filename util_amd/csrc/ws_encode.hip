@@ -529,6 +529,7 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front_kernel(const unsigned c
 // it (every frame has >= 2 wire bytes, so 8 later frames put >= 16 bytes behind a frame's last
 // chunk): those threads add the wire lengths of the frames after theirs. The last tile to finish
 // returns the state to zero (it rests at zero between calls: WsSlot::lookback_state).
+#define ENC_FT 1024      // frames per look-back tile (256: 4,096 tiles for 1 M frames, look-backs 64 tiles deep)
 #define LB_AGG (1ull << 62)
 #define LB_INC (2ull << 62)
 #define LB_VAL ((1ull << 62) - 1)
@@ -537,7 +538,7 @@ __device__ __forceinline__ u64 enc_wirelen(const WebsocketEncodeDesc_t* f, u32 i
     return (u64)enc_hl(len) + (f[i].masked ? 4u : 0u) + len;
 }
 
-__global__ __launch_bounds__(ENC_TILE) void ws_enc_front1_kernel(const unsigned char* __restrict__ src,
+__global__ __launch_bounds__(ENC_FT) void ws_enc_front1_kernel(const unsigned char* __restrict__ src,
                                                                  const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
                                                                  u64* __restrict__ lb, u32 B, u64* __restrict__ wire_off,
                                                                  u32* __restrict__ ptr, u64 npieces,
@@ -545,11 +546,11 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front1_kernel(const unsigned 
     const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     u32* const ctr = reinterpret_cast<u32*>(lb + B);                         // ticket, finished tiles
     __shared__ u32 s_tile, s_last;
-    __shared__ u64 ws[ENC_TILE / 64], s_pre;
+    __shared__ u64 ws[ENC_FT / 64], s_pre;
     if (tid == 0) s_tile = atomicAdd(ctr, 1u);
     __syncthreads();
     const u32 t = s_tile;
-    const u32 i = t * ENC_TILE + tid;
+    const u32 i = t * ENC_FT + tid;
     EncFrame e = {}, nx = {};
     if (i < n) e = enc_load_at(f, i, 0);
     if (i + 1 < n) nx = enc_load_at(f, i + 1, 0);
@@ -560,7 +561,8 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front1_kernel(const unsigned 
     if (wv == 0) {
         // the look-back, by the first wavefront: 64 tiles per step (lane l reads tile t-1-l-64k),
         // summing aggregates back to the nearest tile that has published its inclusive prefix
-        const u64 tsum = ws[0] + ws[1] + ws[2] + ws[3];
+        u64 tsum = 0;
+        for (u32 w = 0; w < ENC_FT / 64; ++w) tsum += ws[w];
         if (lane == 0)
             __hip_atomic_store(lb + t, (t == 0 ? LB_INC : LB_AGG) | tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         u64 pre = 0;
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front1_kernel(const unsigned 
     if (tid == 0) s_last = atomicAdd(ctr + 1, 1u) == B - 1;
     __syncthreads();
     if (s_last) {
-        for (u32 j = tid; j < B; j += ENC_TILE) __hip_atomic_store(lb + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (u32 j = tid; j < B; j += ENC_FT) __hip_atomic_store(lb + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) {
             __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -648,12 +650,12 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     if ((rc = slot.acquire(st))) return rc;
     if (fmode == 1) {
         // one launch: tiles in ticket order, prefix by decoupled look-back
-        const u32 B = (nframes + ENC_TILE - 1) / ENC_TILE;
+        const u32 B = (nframes + ENC_FT - 1) / ENC_FT;
         void* lbp = nullptr;
         if ((rc = slot.lookback_state((size_t)B * 8 + 16, &lbp))) return rc;
         if ((rc = slot.encode_workspace(npieces * 4 + 16, &ws))) return rc;
         ptr = reinterpret_cast<u32*>(ws);
-        hipLaunchKernelGGL(ws_enc_front1_kernel, dim3(B), dim3(ENC_TILE), 0, st, d_src, d_frames, nframes,
+        hipLaunchKernelGGL(ws_enc_front1_kernel, dim3(B), dim3(ENC_FT), 0, st, d_src, d_frames, nframes,
                            reinterpret_cast<u64*>(lbp), B, (u64*)d_wire_off, ptr, npieces, d_dst, (u64)dst_capacity);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("encode front launch", e);
     } else if (front) {
