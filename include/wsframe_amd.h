@@ -219,9 +219,8 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * at least one segment per 8 pieces of 16 KiB, else / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side, default 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
- * fused kernel's window/occupancy), "enc_front" (encode: 1 single-pass look-back front with the
- * edge chunks before the copy, 2 the same front as three launches, 0 hipcub scan and an edge
- * kernel after it), "host_chunk_mb",
+ * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
+ * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:
  * chunk-parallel walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront;
  * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured

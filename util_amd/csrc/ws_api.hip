@@ -86,7 +86,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_reasm_cfg = (int)value;
     }
     else if (!strcmp(name, "enc_front")) {
-        if (value < 0 || value > 2) return -1;
+        if (value < 0 || value > 1) return -1;
         ws_enc_front = (int)value;
     }
     else if (!strcmp(name, "stream_rw")) {
@@ -157,8 +157,6 @@ struct WsStreamWs {
     size_t ws_bytes = 0;
     void* ews = nullptr;           // encode workspace (scan temp + piece pointers)
     size_t ews_bytes = 0;
-    void* lws = nullptr;           // look-back scan state (zero at allocation; every call leaves it zero)
-    size_t lws_bytes = 0;
     void* aws = nullptr;           // auxiliary device scratch (the stream path's chunk-parallel walk)
     size_t aws_bytes = 0;
     void* hws = nullptr;           // ... and its pinned host copy
@@ -186,7 +184,7 @@ size_t ws_workspace_bytes_total() {
     size_t t = 0;
     for (auto& d : g_dev) {
         for (auto& w : d.sw) {
-            t += w.ws_bytes + w.ews_bytes + w.aws_bytes + w.lws_bytes;
+            t += w.ws_bytes + w.ews_bytes + w.aws_bytes;
             for (auto& r : w.retired) t += r.second;
         }
         for (auto& r : d.deferred) t += r.second;
@@ -230,15 +228,14 @@ static bool capturing(hipStream_t stream) {
 static void slot_free(WsStreamWs& w) {
     (void)hipFree(w.ws);
     (void)hipFree(w.ews);
-    (void)hipFree(w.lws);
     (void)hipFree(w.aws);
     if (w.hws) (void)hipHostFree(w.hws);
     if (w.adv_h) (void)hipHostFree(w.adv_h);
     for (auto& r : w.retired) (void)hipFree(r.first);
     w.retired.clear();
-    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr; w.lws = nullptr;
+    w.ws = nullptr; w.ews = nullptr; w.aws = nullptr; w.hws = nullptr; w.hws_dev = nullptr;
     w.adv_h = nullptr; w.adv_d = nullptr;
-    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = w.lws_bytes = 0;
+    w.ws_bytes = w.ews_bytes = w.aws_bytes = w.hws_bytes = 0;
     w.aux_state_ok = false;
     w.stream = nullptr;
     w.capture = 0;
@@ -452,16 +449,6 @@ int WsSlot::workspace(size_t bytes, size_t zero_bytes, void** out) {
     w->ws = reinterpret_cast<u32*>(p);
     if (rc) return rc;
     *out = p;
-    return 0;
-}
-
-// single-pass look-back scan state (ws_encode.hip): zeroed whole at every (re)allocation; each
-// call's last workgroup returns the words it used to zero, so the state rests at zero
-int WsSlot::lookback_state(size_t bytes, void** out) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    const int rc = grow(w, &w->lws, &w->lws_bytes, bytes, st, ~(size_t)0, "hipMalloc(look-back state)");
-    if (rc) return rc;
-    *out = w->lws;
     return 0;
 }
 

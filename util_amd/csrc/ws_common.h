@@ -427,7 +427,6 @@ struct WsSlot {
     void release();
     int workspace(size_t bytes, size_t zero_bytes, void** out);   // decode / reassembly / stream
     int encode_workspace(size_t bytes, void** out);
-    int lookback_state(size_t bytes, void** out);
     int aux(size_t dbytes, size_t hbytes, WsAux* out);
     int advice(int** host, int** dev);                             // the stride hint words (eager)
 };

@@ -520,113 +520,12 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front_kernel(const unsigned c
     enc_edges(src, f, n, i, e, nx, dst, min(all, capacity), enc_fused != 0);
 }
 
-// ---- single-pass front (enc_front 1, round 5): F1 + F2 + F3 in ONE launch. Each 256-frame tile
-// takes a ticket (tiles run in dispatch order), publishes its wire-byte sum, and finds its
-// exclusive prefix by DECOUPLED LOOK-BACK over the tiles before it: one 8-B word per tile,
-// flag (2 bits: 1 aggregate, 2 inclusive prefix) | value (62 bits), stored and polled with
-// agent-scope atomics — a self-contained granule, so no other ordering is needed. The wire total
-// is not known to any tile but the last, and only frames within 8 of the batch's end can need
-// it (every frame has >= 2 wire bytes, so 8 later frames put >= 16 bytes behind a frame's last
-// chunk): those threads add the wire lengths of the frames after theirs. The last tile to finish
-// returns the state to zero (it rests at zero between calls: WsSlot::lookback_state).
-#define ENC_FT 1024      // frames per look-back tile (256: 4,096 tiles for 1 M frames, look-backs 64 tiles deep)
-#define LB_AGG (1ull << 62)
-#define LB_INC (2ull << 62)
-#define LB_VAL ((1ull << 62) - 1)
-__device__ __forceinline__ u64 enc_wirelen(const WebsocketEncodeDesc_t* f, u32 i) {
-    const u64 len = f[i].len;
-    return (u64)enc_hl(len) + (f[i].masked ? 4u : 0u) + len;
-}
-
-__global__ __launch_bounds__(ENC_FT) void ws_enc_front1_kernel(const unsigned char* __restrict__ src,
-                                                                 const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
-                                                                 u64* __restrict__ lb, u32 B, u64* __restrict__ wire_off,
-                                                                 u32* __restrict__ ptr, u64 npieces,
-                                                                 unsigned char* __restrict__ dst, u64 capacity) {
-    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    u32* const ctr = reinterpret_cast<u32*>(lb + B);                         // ticket, finished tiles
-    __shared__ u32 s_tile, s_last;
-    __shared__ u64 ws[ENC_FT / 64], s_pre;
-    if (tid == 0) s_tile = atomicAdd(ctr, 1u);
-    __syncthreads();
-    const u32 t = s_tile;
-    const u32 i = t * ENC_FT + tid;
-    EncFrame e = {}, nx = {};
-    if (i < n) e = enc_load_at(f, i, 0);
-    if (i + 1 < n) nx = enc_load_at(f, i + 1, 0);
-    const u64 wl = i < n ? e.hl + e.len : 0;
-    const u64 incl = enc_wave_incl(wl, lane);
-    if (lane == 63) ws[wv] = incl;
-    __syncthreads();
-    if (wv == 0) {
-        // the look-back, by the first wavefront: 64 tiles per step (lane l reads tile t-1-l-64k),
-        // summing aggregates back to the nearest tile that has published its inclusive prefix
-        u64 tsum = 0;
-        for (u32 w = 0; w < ENC_FT / 64; ++w) tsum += ws[w];
-        if (lane == 0)
-            __hip_atomic_store(lb + t, (t == 0 ? LB_INC : LB_AGG) | tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        u64 pre = 0;
-        for (long long base = (long long)t - 1; base >= 0; base -= 64) {
-            const long long j = base - (long long)lane;
-            u64 w = LB_INC;                                                  // before tile 0: prefix 0
-            if (j >= 0) {
-                // every tile before us took its ticket earlier: it is running or done
-                while (!((w = __hip_atomic_load(lb + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62))
-                    __builtin_amdgcn_s_sleep(1);
-            }
-            const u64 incm = __ballot((w >> 62) == 2);
-            const u32 stop = incm ? (u32)__builtin_ctzll(incm) : 64u;     // the nearest inclusive prefix
-            u64 v = lane <= stop ? (w & LB_VAL) : 0;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor((unsigned long long)v, d, 64);
-            pre += v;
-            if (incm) break;
-        }
-        if (lane == 0) {
-            if (t) __hip_atomic_store(lb + t, LB_INC | (pre + tsum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_pre = pre;
-        }
-    }
-    __syncthreads();
-    u64 off = s_pre + incl - wl;
-    for (u32 w = 0; w < wv; ++w) off += ws[w];
-    if (i < n) {
-        // the batch total, where it can matter (the last 8 frames): this frame's end + the rest
-        u64 all = ~0ull;
-        if (n - 1 - i < 8) {
-            all = off + wl;
-            for (u32 j = i + 1; j < n; ++j) all += enc_wirelen(f, j);
-            if (i == n - 1) wire_off[n] = all;
-        }
-        wire_off[i] = off;
-        e.off = off;
-        nx.off = off + wl;
-        const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
-        // piece pointers (as ws_enc_front_kernel)
-        const u64 a = i ? off + lead0 : 0, b = off + wl + lead0;
-        for (u64 p = (a + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT; (p << ENC_SHIFT) < b && p < npieces; ++p) ptr[p] = i;
-        if (i == n - 1)
-            for (u64 p = (b + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT; p < npieces; ++p) ptr[p] = ENC_NONE;
-        enc_edges(src, f, n, i, e, nx, dst, min(all, capacity), false);
-    }
-    // the last tile to finish its look-back-dependent work returns the state to zero (every other
-    // tile has published and read its words by then: each counts itself done after its look-back)
-    if (tid == 0) s_last = atomicAdd(ctr + 1, 1u) == B - 1;
-    __syncthreads();
-    if (s_last) {
-        for (u32 j = tid; j < B; j += ENC_FT) __hip_atomic_store(lb + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) {
-            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
 // Measured and dropped (round 2): E4 on a side stream, edges fused into E3,
 // E3 over two windows or XCD-contiguous pieces, fewer E3 blocks per CU.
-WsOpt ws_enc_front{1};    // "enc_front": 1 single-pass look-back front (offsets, piece pointers, edge chunks in
-                          // one launch) before E3; 2 the same work as F1-F3 (tile sums, tile scan, one thread
-                          // per frame); 0 hipcub scan + E2, E3, then E4
+WsOpt ws_enc_front{1};    // "enc_front": 1 F1-F3 front (tile sums, tile scan, one thread per frame: offsets,
+                          // piece pointers, edge chunks) before E3; 0 hipcub scan + E2, E3, then E4
+                          // (round 5: F1-F3 as ONE launch with a decoupled look-back over 256- or 1024-frame
+                          // tiles measured no faster, 76 us against 73; not kept)
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned char* d_src,
                                                                   const WebsocketEncodeDesc_t* d_frames,
@@ -639,8 +538,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
     const u64 lead0 = reinterpret_cast<uintptr_t>(d_dst) & 15;
     const u64 npieces = (dst_capacity + lead0 + (1ull << ENC_SHIFT) - 1) >> ENC_SHIFT;
-    const int fmode = ws_enc_front;
-    const bool front = fmode != 0;
+    const bool front = ws_enc_front != 0;
     const u32 fused = 0u;
     hipError_t e;
     int rc;
@@ -648,17 +546,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
     u32* ptr = nullptr;
     WsSlot slot;
     if ((rc = slot.acquire(st))) return rc;
-    if (fmode == 1) {
-        // one launch: tiles in ticket order, prefix by decoupled look-back
-        const u32 B = (nframes + ENC_FT - 1) / ENC_FT;
-        void* lbp = nullptr;
-        if ((rc = slot.lookback_state((size_t)B * 8 + 16, &lbp))) return rc;
-        if ((rc = slot.encode_workspace(npieces * 4 + 16, &ws))) return rc;
-        ptr = reinterpret_cast<u32*>(ws);
-        hipLaunchKernelGGL(ws_enc_front1_kernel, dim3(B), dim3(ENC_FT), 0, st, d_src, d_frames, nframes,
-                           reinterpret_cast<u64*>(lbp), B, (u64*)d_wire_off, ptr, npieces, d_dst, (u64)dst_capacity);
-        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("encode front launch", e);
-    } else if (front) {
+    if (front) {
         // F1 tile sums -> F2 tile scan (also wire_off[n]) -> F3 offsets, piece pointers, edges
         const u32 B = (nframes + ENC_TILE - 1) / ENC_TILE, blocks = B;
         const size_t ptr_off = ((size_t)(B + 1) * 8 + 255) & ~(size_t)255;

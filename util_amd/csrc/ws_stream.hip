@@ -464,7 +464,6 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_STG 4096       // largest staging list per owner (frame offsets); the call's is stgn
 #define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
 #define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
-#define RW_VB 4           // R1: candidates verified per pass (their loads in flight together)
 
 __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
     u64 v = lo;
@@ -542,22 +541,6 @@ __device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool
     return 0;
 }
 
-// rw_step in two halves, so several steps' loads can be issued together: the header words at pos
-// (unconditional; pos clamped into the buffer), then the step on them
-__device__ __forceinline__ void rw_load(uintptr_t origin, u64 len, u64 pos, u64& h0, u64& h1) {
-    const uintptr_t pa = origin + (pos < len ? pos : 0);
-    const gu32x4* q = reinterpret_cast<const gu32x4*>(pa & ~(uintptr_t)15);
-    ws_hdr_from32(q[0], q[1], (u32)(pa & 15), h0, h1);
-}
-__device__ __forceinline__ u32 rw_eval(u64 h0, u64 h1, u64 len, u64& pos, bool need_mask) {
-    if (pos >= len || len - pos < 2) return 1;
-    if (!rw_plausible((u32)h0 & 0xFFu, (u32)(h0 >> 8) & 0xFFu, (u32)(h0 >> 16) & 0xFFFFu, need_mask)) return 2;
-    const WsHdr h = ws_parse(h0, h1, len - pos);
-    if (h.kind != WS_PARSE_FRAME || h.ret <= 0) return 1;
-    pos += (u32)h.ret;
-    return 0;
-}
-
 // R1 (candidates): one thread per RW_TPOS window positions (aligned 16-B loads); the
 // plausible positions of a wavefront are appended to its chunk's list (capc slots) with
 // one atomic per wave on the chunk's counter
@@ -617,34 +600,17 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         rm &= lo >= 64 ? 0ull : ~0ull << lo;
         cands &= rm;
         {
-            // RW_VB candidates per pass with their header loads independent (round 5): the wave
-            // waits for its busiest lane, and one candidate at a time made that 2 dependent loads
-            // per candidate; now 2 per pass of RW_VB
             const u64 cend = cs0 + C;
             u64 keep = cands;
+            // (round 5: four candidates per pass with their header loads issued together measured
+            // slower on cfg3, 8.15-8.19 against 8.10-8.12 ms, profiles/r05_stream_r1_batch_ab.log)
             while (cands) {
-                u32 k[RW_VB];
-                u64 pos[RW_VB];
-                u32 r[RW_VB];
-#pragma unroll
-                for (u32 i = 0; i < RW_VB; ++i) {
-                    k[i] = cands ? (u32)__builtin_ctzll(cands) : 64u;
-                    cands &= cands ? cands - 1 : 0ull;
-                    pos[i] = p0 + (k[i] < 64 ? k[i] : 0u);
-                }
-                u64 h0[RW_VB], h1[RW_VB];
-#pragma unroll
-                for (u32 i = 0; i < RW_VB; ++i) rw_load(origin, len, pos[i], h0[i], h1[i]);
-#pragma unroll
-                for (u32 i = 0; i < RW_VB; ++i) r[i] = rw_eval(h0[i], h1[i], len, pos[i], need_mask);
-#pragma unroll
-                for (u32 i = 0; i < RW_VB; ++i) rw_load(origin, len, pos[i], h0[i], h1[i]);
-#pragma unroll
-                for (u32 i = 0; i < RW_VB; ++i) {
-                    u64 p2 = pos[i];
-                    const bool go = k[i] < 64 && r[i] == 0 && pos[i] < cend;
-                    if (go && rw_eval(h0[i], h1[i], len, p2, need_mask) == 2) keep &= ~(1ull << k[i]);
-                }
+                const u32 k = (u32)__builtin_ctzll(cands);
+                cands &= cands - 1;
+                u64 pos = p0 + k;
+                if (rw_step(origin, len, pos, need_mask) == 0 && pos < cend &&
+                    rw_step(origin, len, pos, need_mask) == 2)
+                    keep &= ~(1ull << k);
             }
             cands = keep;
         }
