@@ -344,7 +344,7 @@ def test_window_mappings(dev, decode_path, opt, val):
         ends = so[1:] + [len(wire)]
         assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d cfg5" % (opt, val))
     finally:
-        W.set_option("piece_win", 1)
+        W.set_option("piece_win", -1)
         W.set_option("seg_win", 1)
         W.set_option("piece_lds", 0)
 

@@ -70,7 +70,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_piece_lds = (int)value;
     }
     else if (!strcmp(name, "piece_win")) {
-        if (value < 0 || value > 6) return -1;
+        if (value < -1 || value > 6) return -1;
         ws_piece_win = (int)value;
     }
     else if (!strcmp(name, "seg_win")) {

@@ -407,7 +407,12 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
             slo = w0 & 0xFFFFFFFFFFFFull; shi = w1 & 0xFFFFFFFFFFFFull;
             cnt = (u32)(w0 >> 48) | ((u32)(w1 >> 48) << 16);
         } else {
-            slo = seg_off[s] + lead0; shi = slo + seg_len[s]; cnt = nwork[s];
+            // (the raw-stream path) the three loads issued together: the compiler would otherwise sink
+            // the second and third below the `slo >= r1` exit, three dependent round trips per wave
+            const u64 so = seg_off[s], sl = seg_len[s];
+            const u32 nw = nwork[s];
+            asm volatile("" ::"s"(so), "s"(sl), "s"(nw));
+            slo = so + lead0; shi = slo + sl; cnt = nw;
         }
         if (!first && slo >= r1) break;                                     // the next segment starts past us
         first = false;
@@ -605,8 +610,8 @@ int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned cha
 // frames keep 6 (cfg3 +0.6 %, cfg4 +0.75 % at 7), 8 loses 2 % (profiles/r04_k2_occupancy_sc1.log).
 // gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
-WsOpt ws_piece_win{1};   // "piece_win": log2 of the number of piece windows K2 streams side by side
-                          // (1: two windows half a batch apart, measured cfg4 74 -> 82 %, cfg2 +2 %, cfg3 =)
+WsOpt ws_piece_win{-1};  // "piece_win": log2 of the number of piece windows K2 streams side by side; -1 (default)
+                          // 2 when the previous call advised frames of one length, else 1 (piece_wshift)
 
 int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0) {
     const int opt = ws_piece_lds;
@@ -661,9 +666,17 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
     return 0;
 }
 
-static u32 piece_wshift(u64 npieces) {
-    const int pwin = ws_piece_win;
-    u32 wshift = (u32)(pwin < 0 ? 0 : (pwin > 6 ? 6 : pwin));
+// Windows: round 1 measured two windows half a batch apart against one (cfg4 74 -> 82 %, cfg2 +2 %,
+// cfg3 =). Round 5 measured the window count per buffer PLACEMENT (several buffers of one config in
+// one process, tools/exp_place_win.py, profiles/r05_place_win.log): one 68.7 GB cfg4 round takes
+// 20.6-22.0 ms with two windows depending on where its buffer lies in HBM, 20.6-21.0 with four
+// (mean -1.6 to -2.2 %, worst buffer -2.7 to -4.8 %, three processes); cfg2 -0.5 % with four; cfg3
+// (mixed lengths) +0.85 % with four. So four windows for batches the previous call advised as frames
+// of one length (g0, the stride hint), two otherwise (first calls, captured calls, mixed lengths).
+static u32 piece_wshift(u64 npieces, u32 g0) {
+    int pwin = ws_piece_win;
+    if (pwin < 0) pwin = g0 >= 2 ? 2 : 1;
+    u32 wshift = (u32)(pwin > 6 ? 6 : pwin);
     while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
     return wshift;
 }
@@ -676,7 +689,7 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     int rc;
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    const u32 wshift = piece_wshift(P.npieces);
+    const u32 wshift = piece_wshift(P.npieces, g0);
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
     if (P.segr)
