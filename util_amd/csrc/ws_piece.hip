@@ -314,13 +314,12 @@ __device__ __forceinline__ void walk_group(const WalkArgs& A, u32 s, bool active
 // K1: one walk per segment (16 lanes each); counts the segments whose frames are not all of one
 // length for the K2 that follows (nonuni, may be null)
 #define PSCAN_T 256
-template <int ST = 15>
 __global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel(WalkArgs A, u32* nonuni) {
     const u32 lane = threadIdx.x & 63;
     const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / WALK_G;
     u32 cnt = 0;
     bool nonu = false;
-    walk_group<ST>(A, s, s < A.nseg, lane, cnt, nonu);
+    walk_group(A, s, s < A.nseg, lane, cnt, nonu);
     if (nonuni) {                                                           // one atomic per wave, if any
         const u64 b = __ballot(lane % WALK_G == 0 && s < A.nseg && nonu);
         if (lane == 0 && b) atomicAdd(nonuni, (u32)__popcll(b));
@@ -561,7 +560,7 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
     PieceWs P;
     const WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
     const u32 blocks = (u32)(((u64)L.nseg * WALK_G + PSCAN_T - 1) / PSCAN_T);
-    hipLaunchKernelGGL(ws_piece_scan_kernel<15>, dim3(blocks), dim3(PSCAN_T), 0, L.stream, W,
+    hipLaunchKernelGGL(ws_piece_scan_kernel, dim3(blocks), dim3(PSCAN_T), 0, L.stream, W,
                        count_nonuniform ? P.nonuni : nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_scan_kernel launch", e);
@@ -573,6 +572,14 @@ int ws_launch_piece_scan(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u
 // Measurement build only (tools/exp_k1k2.sh compiles this file a second time with it): K1 with a
 // subset of its stores (st: the walk_group ST bitmask) or, st = 16, all stores at 8 waves per SIMD
 // — the K1 breakdown of round 5. Not in the drop-in library.
+template <int ST>
+__global__ __launch_bounds__(PSCAN_T) void ws_piece_scan_kernel_st(WalkArgs A, u32* nonuni) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 s = (blockIdx.x * PSCAN_T + threadIdx.x) / WALK_G;
+    u32 cnt = 0;
+    bool nonu = false;
+    walk_group<ST>(A, s, s < A.nseg, lane, cnt, nonu);
+}
 __global__ __launch_bounds__(PSCAN_T) __attribute__((amdgpu_waves_per_eu(8, 8))) void ws_piece_scan_kernel_w8(
     WalkArgs A, u32* nonuni) {
     const u32 lane = threadIdx.x & 63;
@@ -587,13 +594,13 @@ int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned cha
     const WalkArgs W = piece_scan_args(L, lo, hi, ws, gen, P, g0);
     const dim3 g((u32)(((u64)L.nseg * WALK_G + PSCAN_T - 1) / PSCAN_T)), b(PSCAN_T);
     switch (st) {
-    case 0: hipLaunchKernelGGL(ws_piece_scan_kernel<0>, g, b, 0, L.stream, W, nullptr); break;
-    case 1: hipLaunchKernelGGL(ws_piece_scan_kernel<1>, g, b, 0, L.stream, W, nullptr); break;
-    case 3: hipLaunchKernelGGL(ws_piece_scan_kernel<3>, g, b, 0, L.stream, W, nullptr); break;
-    case 7: hipLaunchKernelGGL(ws_piece_scan_kernel<7>, g, b, 0, L.stream, W, nullptr); break;
-    case 8: hipLaunchKernelGGL(ws_piece_scan_kernel<8>, g, b, 0, L.stream, W, nullptr); break;
-    case 13: hipLaunchKernelGGL(ws_piece_scan_kernel<13>, g, b, 0, L.stream, W, nullptr); break;
-    case 15: hipLaunchKernelGGL(ws_piece_scan_kernel<15>, g, b, 0, L.stream, W, nullptr); break;
+    case 0: hipLaunchKernelGGL(ws_piece_scan_kernel_st<0>, g, b, 0, L.stream, W, nullptr); break;
+    case 1: hipLaunchKernelGGL(ws_piece_scan_kernel_st<1>, g, b, 0, L.stream, W, nullptr); break;
+    case 3: hipLaunchKernelGGL(ws_piece_scan_kernel_st<3>, g, b, 0, L.stream, W, nullptr); break;
+    case 7: hipLaunchKernelGGL(ws_piece_scan_kernel_st<7>, g, b, 0, L.stream, W, nullptr); break;
+    case 8: hipLaunchKernelGGL(ws_piece_scan_kernel_st<8>, g, b, 0, L.stream, W, nullptr); break;
+    case 13: hipLaunchKernelGGL(ws_piece_scan_kernel_st<13>, g, b, 0, L.stream, W, nullptr); break;
+    case 15: hipLaunchKernelGGL(ws_piece_scan_kernel_st<15>, g, b, 0, L.stream, W, nullptr); break;
     case 16: hipLaunchKernelGGL(ws_piece_scan_kernel_w8, g, b, 0, L.stream, W, nullptr); break;
     default: return -1;
     }
@@ -611,7 +618,8 @@ int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned cha
 // gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{-1};  // "piece_win": log2 of the number of piece windows K2 streams side by side; -1 (default)
-                          // 2 when the previous call advised frames of one length, else 1 (piece_wshift)
+                          // 2 for batches of >= 16 GiB the previous call advised as frames of one length, else 1
+                          // (piece_wshift)
 
 int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0) {
     const int opt = ws_piece_lds;
@@ -671,11 +679,15 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
 // one process, tools/exp_place_win.py, profiles/r05_place_win.log): one 68.7 GB cfg4 round takes
 // 20.6-22.0 ms with two windows depending on where its buffer lies in HBM, 20.6-21.0 with four
 // (mean -1.6 to -2.2 %, worst buffer -2.7 to -4.8 %, three processes); cfg2 -0.5 % with four; cfg3
-// (mixed lengths) +0.85 % with four. So four windows for batches the previous call advised as frames
-// of one length (g0, the stride hint), two otherwise (first calls, captured calls, mixed lengths).
+// (mixed lengths) +0.85 % with four. In the bench's own protocol (the same buffer re-decoded) cfg2
+// runs 0.4 % slower with four (1.3597-1.3623 against 1.3539-1.3545 ms at 100 steps, processes
+// paired over both placements, profiles/r05_win_ab.log) while cfg4 keeps the gain. So four windows
+// for batches of >= 1 M pieces (16 GiB) the previous call advised as frames of one length (g0, the
+// stride hint), two otherwise (first calls, captured calls, mixed lengths, smaller batches).
+#define PIECE_WIN4_MIN (1ull << 20)
 static u32 piece_wshift(u64 npieces, u32 g0) {
     int pwin = ws_piece_win;
-    if (pwin < 0) pwin = g0 >= 2 ? 2 : 1;
+    if (pwin < 0) pwin = g0 >= 2 && npieces >= PIECE_WIN4_MIN ? 2 : 1;
     u32 wshift = (u32)(pwin > 6 ? 6 : pwin);
     while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
     return wshift;
