@@ -18,6 +18,8 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 wins = [int(x) for x in os.environ.get("EXP_WIN", "1,2").split(",")]
+opt = os.environ.get("EXP_OPT", "piece_win")                  # seg_win: the segment kernels (cfg5)
+dflt = {"piece_win": -1, "seg_win": 1}.get(opt, 0)
 dev = torch.device("cuda", 0)
 wls = [bench.Workload.make(cfg, dev) for _ in range(K)]
 torch.cuda.synchronize()
@@ -25,7 +27,7 @@ out = {"config": cfg, "buffers": [hex(w.buf.data_ptr()) for w in wls], "ms": {}}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(rounds):
     for win in wins:
-        W.set_option("piece_win", win)
+        W.set_option(opt, win)
         for k, w in enumerate(wls):
             for _ in range(2):
                 W.batch_decode_device(w.buf, w.seg_off, w.seg_len, w.fps, w.desc, w.res)
@@ -36,5 +38,5 @@ for r in range(rounds):
             e1.record()
             torch.cuda.synchronize()
             out["ms"].setdefault("buf%d_win%d" % (k, win), []).append(round(e0.elapsed_time(e1) / iters, 4))
-W.set_option("piece_win", -1)
+W.set_option(opt, dflt)
 print(json.dumps(out))
