@@ -18,6 +18,7 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 wins = [int(x) for x in os.environ.get("EXP_WIN", "0,1,2").split(",")]
+opt = os.environ.get("EXP_OPT", "enc_win")                    # or enc_xg
 dev = torch.device("cuda", 0)
 wls = [bench.EncodeWorkload(cfg, dev, seed_offset=k) for k in range(K)]
 torch.cuda.synchronize()
@@ -25,7 +26,7 @@ out = {"config": cfg, "ms": {}}
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for r in range(rounds):
     for win in wins:
-        W.set_option("enc_win", win)
+        W.set_option(opt, win)
         for k, w in enumerate(wls):
             for _ in range(2):
                 w.step()
@@ -36,6 +37,6 @@ for r in range(rounds):
             e1.record()
             torch.cuda.synchronize()
             out["ms"].setdefault("wl%d_win%d" % (k, win), []).append(round(e0.elapsed_time(e1) / iters, 4))
-W.set_option("enc_win", 0)
+W.set_option(opt, 0)
 assert all(w.verify() == 0 for w in wls)
 print(json.dumps(out))

@@ -31,6 +31,7 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_enc_win;
+extern WsOpt ws_enc_xg;
 extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
@@ -85,6 +86,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "reasm_cfg")) {
         if (value < 0 || value > 2) return -1;
         ws_reasm_cfg = (int)value;
+    }
+    else if (!strcmp(name, "enc_xg")) {
+        if (value < 0 || value > 1) return -1;
+        ws_enc_xg = (int)value;
     }
     else if (!strcmp(name, "enc_win")) {
         if (value < 0 || value > 3) return -1;
