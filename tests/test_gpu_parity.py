@@ -325,7 +325,7 @@ def test_int_truncation_real_size(dev, decode_path, total):
     del gb, ob, host
 
 
-@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("piece_dir", 1), ("seg_win", 0),
+@pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0),
                                      ("piece_lds", 1), ("piece_lds", 56000)])
 def test_window_mappings(dev, decode_path, opt, val):
     """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
@@ -345,7 +345,6 @@ def test_window_mappings(dev, decode_path, opt, val):
         assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d cfg5" % (opt, val))
     finally:
         W.set_option("piece_win", -1)
-        W.set_option("piece_dir", 0)
         W.set_option("seg_win", 1)
         W.set_option("piece_lds", 0)
 

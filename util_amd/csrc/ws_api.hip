@@ -26,7 +26,6 @@ extern WsOpt ws_reasm_path;
 extern WsOpt ws_reasm_cfg;
 extern WsOpt ws_piece_lds;
 extern WsOpt ws_piece_win;
-extern WsOpt ws_piece_dir;
 extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
@@ -71,10 +70,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "piece_lds")) {
         if (value < 0 || value > 65536) return -1;
         ws_piece_lds = (int)value;
-    }
-    else if (!strcmp(name, "piece_dir")) {
-        if (value < 0 || value > 1) return -1;
-        ws_piece_dir = (int)value;
     }
     else if (!strcmp(name, "piece_win")) {
         if (value < -1 || value > 6) return -1;

@@ -350,11 +350,9 @@ __global__ __launch_bounds__(PIECE_T) void ws_piece_unmask_kernel(unsigned char*
     // (block b takes piece (b mod W) * ppw + b / W); blocks past the last piece load a
     // clamped piece and store nothing
     const u32 bx = blockIdx.x;
-    // (wshift bit 8, option piece_dir: odd windows are streamed from their end, so two windows'
-    // distance sweeps every value instead of staying one batch fraction)
-    const u32 wsh = wshift & 255u, wi = bx & ((1u << wsh) - 1u);
-    const u64 ib = bx >> wsh;
-    const u64 pw = (wshift >> 8) && (wi & 1u) ? (u64)(wi + 1) * ppw - 1 - ib : (u64)wi * ppw + ib;
+    // (round 5: odd windows streamed from their end measured +0.15 % on cfg2 and +0.7 % on cfg3,
+    // profiles/r05_piece_dir_place.log)
+    const u64 pw = (u64)(bx & ((1u << wshift) - 1u)) * ppw + (bx >> wshift);
     const bool pvalid = pw < npieces;
     const u64 pidx = pvalid ? pw : npieces - 1;
     const u64 pc0 = (pbase + pidx) << (PIECE_SHIFT - 4);                     // first chunk of the piece
@@ -621,7 +619,6 @@ int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned cha
 // frames keep 6 (cfg3 +0.6 %, cfg4 +0.75 % at 7), 8 loses 2 % (profiles/r04_k2_occupancy_sc1.log).
 // gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
-WsOpt ws_piece_dir{0};   // "piece_dir": 1 odd piece windows streamed from their end (placement experiment)
 WsOpt ws_piece_win{-1};  // "piece_win": log2 of the number of piece windows K2 streams side by side; -1 (default)
                           // 2 for batches of >= 16 GiB the previous call advised as frames of one length, else 1
                           // (piece_wshift)
@@ -709,16 +706,15 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const u32 wshift = piece_wshift(P.npieces, g0);
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
-    const u32 wsarg = wshift | (ws_piece_dir && wshift ? 256u : 0u);
     if (P.segr)
         hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 1>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
-                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wsarg, ppw, (u64)P.npieces, P.nonuni,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)P.segr);
     else
         hipLaunchKernelGGL((ws_piece_unmask_kernel<4, 0>), dim3((u32)grid), dim3(PIECE_T), ws_piece_dyn_lds(L, P.npieces, g0), L.stream,
                            L.buf, L.seg_off, L.seg_len, L.nseg, L.max_frames, P.items, P.nwork, P.ptr, P.disorder, gen,
-                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wsarg, ppw, (u64)P.npieces, P.nonuni,
+                           P.pbase, P.c_lo, P.c_hi, L.desc_base, L.desc, L.res, wshift, ppw, (u64)P.npieces, P.nonuni,
                            advice, (const WsSegRec*)nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return ws_set_err("ws_piece_unmask_kernel launch", e);
