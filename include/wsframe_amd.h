@@ -221,13 +221,10 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * the stream advised as frames of one length, else 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
- * chunks before the copy, 0 hipcub scan and an edge kernel after it), "enc_win" (0..3: log2 of the
- * output-piece windows the encode copy streams side by side, default 0), "enc_xg" (1: within every 32
- * copy blocks, the four on one XCD take four consecutive output pieces; default 0), "host_chunk_mb",
- * "stream_rw" / "stream_rw_cmax" / "stream_rw_hm" / "stream_rounds" / "stream_plink" (raw stream:
+ * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
+ * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:
  * chunk-parallel walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront;
- * log2 of its largest chunk 16..26, its chunk windows' length in mean frames 0..16 (at least the
- * longest frame seen + 4 KiB; default 4), pass rounds of a captured call 1..64, a captured
+ * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
  * call's chunk records linked in parallel 0/1), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */

@@ -153,32 +153,3 @@ def test_encode_many_tiles(dev):
         assert np.array_equal(got, np.frombuffer(want, dtype=np.uint8))
         assert (out[:shift] == 0xA5).all() and (out[shift + len(want):] == 0xA5).all()
 
-
-@pytest.mark.parametrize("ewin,xg", [(1, 0), (2, 0), (3, 0), (0, 1), (1, 1)])
-def test_encode_copy_windows(dev, ewin, xg):
-    """the copy kernel over 2^ewin output-piece windows (option enc_win; the grid rounds up to
-    W * ceil(P / W), spare blocks store nothing) on a batch of > 2,048 pieces of 16 KiB, so every
-    window is used: bit-exact vs the oracle, nothing written past the wire"""
-    rng = np.random.default_rng(20 + ewin)
-    n = 6000
-    lens = rng.integers(4000, 9000, n)
-    src = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
-    fr = np.zeros(n, W.ENC_DTYPE)
-    fr["src_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
-    fr["len"] = lens
-    fr["mask_key"] = rng.integers(0, 2**32, n, dtype=np.uint64)
-    fr["type"] = 2
-    fr["is_fin"] = 1
-    fr["prev_is_fin"] = 1
-    fr["masked"] = 1
-    want, woff = oracle_encode_frames(src, fr)
-    W.set_option("enc_win", ewin)
-    W.set_option("enc_xg", xg)
-    try:
-        out, off = gpu_encode(dev, src, fr, dst_shift=3)
-    finally:
-        W.set_option("enc_win", 0)
-        W.set_option("enc_xg", 0)
-    assert np.array_equal(off, woff)
-    assert np.array_equal(out[3:3 + len(want)], np.frombuffer(want, dtype=np.uint8))
-    assert (out[:3] == 0xA5).all() and (out[3 + len(want):] == 0xA5).all()

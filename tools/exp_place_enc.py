@@ -1,7 +1,9 @@
 """Experiment only (placement): K encode workloads of one config in ONE process
 (each its own source and wire buffers), every (enc_win, workload) pair timed with `iters`
 back-to-back encode calls, rounds interleaved.
-    GPU box: python tools/exp_place_enc.py [config] [K] [rounds] [iters]   (EXP_WIN=0,1,2)"""
+    GPU box: python tools/exp_place_enc.py [config] [K] [rounds] [iters]   (EXP_WIN=0,1,2)
+The swept options (enc_win, enc_xg) were removed from the library after the measurement (round 5,
+commit ff92800 has them): EXP_OPT=enc_front still works."""
 import json
 import os
 import sys

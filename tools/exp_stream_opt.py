@@ -1,7 +1,9 @@
 """Experiment only: raw-stream decode of one config's wire (ONE buffer, so one placement) with an
 option alternated in-process: `iters` calls per (value, round), rounds interleaved; also the
 calls' chunk-walk stats.
-    GPU box: python tools/exp_stream_opt.py <config> <option> <v1,v2,...> [rounds] [iters]"""
+    GPU box: python tools/exp_stream_opt.py <config> <option> <v1,v2,...> [rounds] [iters]
+(round 5 swept stream_rw_cmax and stream_rw_hm; the latter was removed after it measured neutral,
+commit fcd51c2 has it)"""
 import json
 import os
 import sys

@@ -30,11 +30,9 @@ extern WsOpt ws_k2_timing;
 void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
-extern WsOpt ws_enc_win;
-extern WsOpt ws_enc_xg;
 extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
-extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink, ws_stream_rw_hm;
+extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips;
 extern std::atomic<unsigned long long> ws_stat_adoptions;
@@ -87,14 +85,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 0 || value > 2) return -1;
         ws_reasm_cfg = (int)value;
     }
-    else if (!strcmp(name, "enc_xg")) {
-        if (value < 0 || value > 1) return -1;
-        ws_enc_xg = (int)value;
-    }
-    else if (!strcmp(name, "enc_win")) {
-        if (value < 0 || value > 3) return -1;
-        ws_enc_win = (int)value;
-    }
     else if (!strcmp(name, "enc_front")) {
         if (value < 0 || value > 1) return -1;
         ws_enc_front = (int)value;
@@ -110,10 +100,6 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_plink")) {
         if (value < 0 || value > 1) return -1;
         ws_stream_plink = (int)value;
-    }
-    else if (!strcmp(name, "stream_rw_hm")) {
-        if (value < 0 || value > 16) return -1;
-        ws_stream_rw_hm = (int)value;
     }
     else if (!strcmp(name, "stream_rounds")) {
         if (value < 1 || value > 64) return -1;

@@ -234,14 +234,12 @@ __global__ __launch_bounds__(ENC_T) void ws_enc_copy_kernel(const unsigned char*
                                                             const WebsocketEncodeDesc_t* __restrict__ f, u32 n,
                                                             const u64* __restrict__ wire_off,
                                                             const u32* __restrict__ ptr, unsigned char* __restrict__ dst,
-                                                            u64 capacity, u32 npieces, u32 ewin, u32 ppw, u32 xg) {
+                                                            u64 capacity, u32 npieces) {
     const u32 tid = threadIdx.x, lane = tid & 63;
-    // output piece: 2^ewin windows of ppw pieces streamed side by side (block b -> piece
-    // (b mod W) * ppw + b / W; ewin 0: block b -> piece b). xg: within every 32 consecutive
-    // blocks, the four that run on one XCD (block b on XCD b mod 8) take four consecutive pieces,
-    // so a frame record spanning them is fetched into one L2
-    const u32 bq = xg ? ((blockIdx.x >> 5) << 5) + ((blockIdx.x & 7u) << 2) + ((blockIdx.x >> 3) & 3u) : blockIdx.x;
-    const u32 pb = (bq & ((1u << ewin) - 1u)) * ppw + (bq >> ewin);
+    // output piece: block b -> piece b. Measured and not kept (round 5): 2-8 windows
+    // (+0.6-2 %), the four blocks of every 32 on one XCD taking consecutive pieces (+0.8 %, though
+    // E3's read over-fetch drops 1.036 -> 1.017 x)
+    const u32 pb = blockIdx.x;
     if (pb >= npieces) return;                                               // the spare blocks
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 lead0 = reinterpret_cast<uintptr_t>(dst) & 15;
@@ -523,8 +521,6 @@ __global__ __launch_bounds__(ENC_TILE) void ws_enc_front_kernel(const unsigned c
 
 // Measured and dropped (round 2): E4 on a side stream, edges fused into E3,
 // E3 over two windows or XCD-contiguous pieces, fewer E3 blocks per CU.
-WsOpt ws_enc_win{0};
-WsOpt ws_enc_xg{0};       // "enc_xg": 1 the copy kernel's blocks take their XCD's four consecutive pieces      // "enc_win": log2 of the output-piece windows E3 streams side by side (0..3)
 WsOpt ws_enc_front{1};    // "enc_front": 1 F1-F3 front (tile sums, tile scan, one thread per frame: offsets,
                           // piece pointers, edge chunks) before E3; 0 hipcub scan + E2, E3, then E4
                           // (round 5: F1-F3 as ONE launch with a decoupled look-back over 256- or 1024-frame
@@ -579,13 +575,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchEncodeDevice(const unsigned
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_ptr_kernel launch", e);
     }
     if (npieces) {
-        u32 ewin = (u32)(int)ws_enc_win;
-        while (ewin && (npieces >> ewin) < 256) --ewin;                      // small batches: one window
-        u64 ppw = (npieces + (1ull << ewin) - 1) >> ewin;
-        if (ws_enc_xg) ppw = (ppw + 31) & ~31ull;                            // whole groups of 32 blocks per window
-        hipLaunchKernelGGL((ws_enc_copy_kernel<1, 0>), dim3((u32)(ppw << ewin)), dim3(ENC_T), 0, st, d_src, d_frames,
-                           nframes, d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces, ewin, (u32)ppw,
-                           ws_enc_xg ? 1u : 0u);
+        hipLaunchKernelGGL((ws_enc_copy_kernel<1, 0>), dim3((u32)npieces), dim3(ENC_T), 0, st, d_src, d_frames,
+                           nframes, d_wire_off, ptr, d_dst, (u64)dst_capacity, (u32)npieces);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_enc_copy_kernel launch", e);
     }
     if (front) return 0;

@@ -476,9 +476,10 @@ __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
 // larger, in 4 KiB steps, within [RW_HMIN, min(C / 2, RW_HMAX)] (round 3: 8 mean frames
 // rounded up to a power of two; cfg3 128 -> 92 KiB, stream 8.32-8.36 -> 8.19 ms eager,
 // profiles/r04_stream_rw_ab.log)
-__device__ static u32 rw_window(u64 mean, u32 maxlen, u64 C, u32 hm) {
+__device__ static u32 rw_window(u64 mean, u32 maxlen, u64 C) {
+    // (round 5: 0, 2 or 4 mean frames measured the same on one buffer, R1 unchanged at 247 us)
     const u64 hi = C / 2 < RW_HMAX ? C / 2 : RW_HMAX;
-    u64 h = mean * hm > (u64)maxlen + 4096 ? mean * hm : (u64)maxlen + 4096;
+    u64 h = mean * 4 > (u64)maxlen + 4096 ? mean * 4 : (u64)maxlen + 4096;
     h = (h + 4095) & ~4095ull;
     return (u32)(h < RW_HMIN ? RW_HMIN : (h > hi ? hi : h));
 }
@@ -801,7 +802,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
-                                                        SdMirror* __restrict__ mirror, u32 hm) {
+                                                        SdMirror* __restrict__ mirror) {
     const u32 lane = threadIdx.x;
     const u32 seen = plan->seen_max;        // the previous walk's longest frame (0 before the first: WS_AUX_ZERO)
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     u64 nch = (len - P1 + C - 1) / C;
     // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
     while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
-    const u32 H = rw_window(mean, o.maxlen > seen ? o.maxlen : seen, C, hm);
+    const u32 H = rw_window(mean, o.maxlen > seen ? o.maxlen : seen, C);
     u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
     while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
     u64 capc = H / 32;
@@ -1184,7 +1185,6 @@ WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long str
                                 // (1) or by the host (2, eager calls), 0 one wavefront
 WsOpt ws_stream_rw_cmax{22};    // "stream_rw_cmax": log2 of the largest chunk (cfg3: 4 MiB 8.11-8.13 ms
                                 // against 8.19-8.21 at 8 MiB and 8.14-8.15 at 2 MiB, profiles/r04_stream_cmax_ab.log)
-WsOpt ws_stream_rw_hm{4};       // "stream_rw_hm": the chunk windows cover max(hm mean frames, the longest + 4 KiB)
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
@@ -1426,7 +1426,7 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
-                       fresh, d_seg, Pw.disorder, mirror, (u32)(int)ws_stream_rw_hm);
+                       fresh, d_seg, Pw.disorder, mirror);
     // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
     hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        cand, nrec, 0u, (const RwPlan*)plan);
