@@ -464,6 +464,7 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_STG 4096       // largest staging list per owner (frame offsets); the call's is stgn
 #define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
 #define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
+#define RW_WCAP 256       // R1: candidates of a wave spread over its lanes (more: lane by lane)
 
 __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
     u64 v = lo;
@@ -559,6 +560,7 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         capc = plan->capc;
     }
     const u32 lane = threadIdx.x & 63;
+    __shared__ unsigned short s_cand[256 / 64][RW_WCAP];                     // a wave's candidates (position in its 4 KiB)
     const u32 per = H / RW_TPOS;                                             // a multiple of 64: one
     // grid-stride (a captured call's grid is sized for the largest geometry); a whole
     // wavefront takes the same iterations
@@ -600,22 +602,12 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         u64 rm = hi >= 64 ? ~0ull : (1ull << hi) - 1;
         rm &= lo >= 64 ? 0ull : ~0ull << lo;
         cands &= rm;
-        {
-            const u64 cend = cs0 + C;
-            u64 keep = cands;
-            // (round 5: four candidates per pass with their header loads issued together measured
-            // slower on cfg3, 8.15-8.19 against 8.10-8.12 ms, profiles/r05_stream_r1_batch_ab.log)
-            while (cands) {
-                const u32 k = (u32)__builtin_ctzll(cands);
-                cands &= cands - 1;
-                u64 pos = p0 + k;
-                if (rw_step(origin, len, pos, need_mask) == 0 && pos < cend &&
-                    rw_step(origin, len, pos, need_mask) == 2)
-                    keep &= ~(1ull << k);
-            }
-            cands = keep;
-        }
     }
+    // Each candidate is checked by its frame and the header after it (two dependent loads). Round 4
+    // did that per lane, so a wave waited for its busiest lane's chain (≈ 5-6 candidates of 64
+    // positions); round 5 spreads the wave's candidates over its 64 lanes through LDS, so a wave
+    // takes ceil(candidates / 64) chains (round 4's per-lane batching of four measured no faster).
+    const u32 wv = threadIdx.x >> 6;
     const u32 n = (u32)__builtin_popcountll(cands);
     u32 incl = n;                                                            // wavefront inclusive scan
 #pragma unroll
@@ -624,17 +616,49 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         if (lane >= d) incl += v;
     }
     const u32 total = (u32)__shfl((int)incl, 63);
-    u32 base = 0;
-    if (lane == 63 && total) base = atomicAdd(nrec + 4 * c + 2, total);    // the chunk's counter
-    base = (u32)__shfl((int)base, 63);
-    u32 o = base + incl - n;
-    u64* cl = cand + c * capc;
-    while (cands) {
-        const u32 k = (u32)__builtin_ctzll(cands);
-        cands &= cands - 1;
-        if (o < capc) cl[o] = a + k - origin;
-        ++o;
+    u64 rest = cands;                                                        // not staged (overflow)
+    for (u32 o = incl - n; rest && o < RW_WCAP; ++o) {
+        s_cand[wv][o] = (unsigned short)((lane << 6) | (u32)__builtin_ctzll(rest));
+        rest &= rest - 1;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const u64 pw0 = (a - origin) - (u64)lane * RW_TPOS;                      // lane 0's first position
+    const u64 cend = cs0 + C;
+    u64* cl = cand + c * capc;
+    const u32 staged = total < RW_WCAP ? total : RW_WCAP;
+    // one verdict per lane per pass: survivors appended to the chunk's list (one atomic per pass)
+    auto verdict = [&](bool have, u64 pos0) {
+        bool keep = false;
+        if (have) {
+            u64 pos = pos0;
+            keep = !(rw_step(origin, len, pos, need_mask) == 0 && pos < cend &&
+                     rw_step(origin, len, pos, need_mask) == 2);
+        }
+        const u64 km = __ballot(keep);
+        const u32 cnt = (u32)__builtin_popcountll(km);
+        u32 ob = 0;
+        if (lane == 0 && cnt) ob = atomicAdd(nrec + 4 * c + 2, cnt);         // the chunk's counter
+        ob = (u32)__shfl((int)ob, 0);
+        if (keep) {
+            const u32 o = ob + (u32)__builtin_popcountll(km & ((1ull << lane) - 1));
+            if (o < capc) cl[o] = pos0;
+        }
+    };
+    for (u32 r = 0; r < staged; r += 64) {
+        const u32 idx = r + lane;
+        const bool have = idx < staged;
+        verdict(have, have ? pw0 + s_cand[wv][idx] : 0);
+    }
+    // a wave with more than RW_WCAP candidates: the rest lane by lane
+    while (__ballot(rest != 0)) {
+        const bool have = rest != 0;
+        const u32 k = have ? (u32)__builtin_ctzll(rest) : 0u;
+        rest &= rest ? rest - 1 : 0ull;
+        verdict(have, (a - origin) + k);
+    }
+    __builtin_amdgcn_wave_barrier();                                         // s_cand reads before the next pass's writes
     }
 }
 
