@@ -176,6 +176,24 @@ def test_long_stream_unmasked_and_mixed(dev):
     run(dev, long_stream(np.random.default_rng(25), 24 << 20, mix3, masked=0.7), 1 << 14)
 
 
+@pytest.mark.parametrize("kind", ["server_zeros", "client_0x80", "partly_dense"])
+def test_long_stream_dense_candidates(dev, kind):
+    """payloads whose every position reads as a plausible header (zero bytes in a server
+    stream, 0x80 bytes in a client one): R1's waves with more candidates than they stage
+    (RW_WCAP) and chunk lists with more survivors than slots"""
+    pick = lambda g: g.integers(2000, 40000)
+    if kind == "server_zeros":
+        wire = long_stream(np.random.default_rng(31), 20 << 20, pick, masked=0.0, payload=lambda g, n: bytes(n))
+    elif kind == "client_0x80":
+        wire = long_stream(np.random.default_rng(32), 20 << 20, pick, masked=1.0, payload=lambda g, n: b"\x80" * n)
+    else:
+        def some(g, n):
+            return b"\x80" * n if g.random() < 0.3 else g.integers(0, 256, n, dtype=np.uint8).tobytes()
+        wire = long_stream(np.random.default_rng(33), 20 << 20, pick, masked=1.0, payload=some)
+    r = run(dev, wire, 1 << 14)
+    assert int(r["consumed"]) == len(wire)
+
+
 def test_long_stream_nested_frames(dev):
     """payloads made of valid client frames: speculative walks that look like the chain
     (slot overflow, merged walks) must not change the result"""
