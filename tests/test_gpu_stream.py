@@ -329,6 +329,27 @@ def test_stream_tiny_frames_medium(dev):
     assert int(r["consumed"]) == len(wire)
 
 
+@pytest.mark.parametrize("alphabet", [(125, 1500, 65536), (7, 300), (0, 126, 65535, 70000)])
+def test_stream_walk_alphabets(dev, alphabet):
+    """the one-wavefront group walk's length speculation (two lengths: a 6-deep tree, three: 4
+    deep, a fourth length replacing one round-robin): short streams of lengths drawn from an
+    alphabet, cut by max_frames at every depth of a step, truncated mid-frame and with a bad
+    header mid-stream"""
+    rng = np.random.default_rng(sum(alphabet))
+    pick = lambda g: g.choice(alphabet)
+    wire = long_stream(rng, 300 << 10, pick, masked=1.0)
+    r = run(dev, wire, 1 << 14)
+    n = int(r["n_frames"])
+    assert int(r["consumed"]) == len(wire)
+    for mf in (1, 2, 3, 4, 5, 6, 7, 11, 13, n // 2, n - 1):
+        r = run(dev, wire, max(1, mf))
+        assert int(r["n_frames"]) == min(mf, n)
+    run(dev, wire[:len(wire) - 3], 1 << 14)                                 # the last frame incomplete
+    bad = wire.copy()
+    bad[len(bad) // 2:len(bad) // 2 + 64] = 0x70                            # RSV bits: a decode error or garbage
+    run(dev, bad, 1 << 14)
+
+
 def test_stream_state_survives_mixed_calls(dev):
     """the pass loop's state rests in the stream's auxiliary workspace between calls: long
     changing streams (the chunk-parallel walk grows that workspace), short ones (the walk in

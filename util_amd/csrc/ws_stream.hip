@@ -464,6 +464,11 @@ __global__ __launch_bounds__(64) void ws_rw_chunk_kernel(const unsigned char* __
 #define RW_STG 4096       // largest staging list per owner (frame offsets); the call's is stgn
 #define RW_MIN (512ull << 10)     // streams shorter than this after the passes: one wavefront walks
 #define RW_MIN_FRAMES 256         // ... and, after the sample, fewer frames than this (by the mean)
+// captured (device-planned) calls: R1 and R2 grid-stride grids, blocks of 256 (round 5: R1
+// 4096 -> 16384 blocks 176.8 -> 160.8 us, R2 4096 -> 8192 42.9 -> 36.9 us on cfg3,
+// profiles/r05_stream_grid_ab.log)
+#define RW_R1_GRID 16384
+#define RW_R2_GRID 8192
 #define RW_WCAP 256       // R1: candidates of a wave spread over its lanes (more: lane by lane)
 
 __host__ __device__ static u64 rw_pow2_clamp(u64 x, u64 lo, u64 hi) {
@@ -1452,9 +1457,9 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
                        fresh, d_seg, Pw.disorder, mirror);
     // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
-    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(RW_R1_GRID), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        cand, nrec, 0u, (const RwPlan*)plan);
-    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(4096), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
+    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(RW_R2_GRID), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
                        (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
     hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len,
                        (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
