@@ -87,7 +87,7 @@ def timed_region(step, steps, world):
     return time.perf_counter() - t0, e0.elapsed_time(e1) / steps
 
 
-def pmc_traffic(kernel, algo_bytes, metric):
+def pmc_traffic(kernel, algo_bytes, metric, graph=None):
     """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this kernel,
     workload and bench metric (profiles/<tag>_pmc.json, tools/prof_summary.py), else None.
     The metric keeps one op's profile from standing in for another op's that runs the same
@@ -99,8 +99,12 @@ def pmc_traffic(kernel, algo_bytes, metric):
             rec = json.load(open(f))
         except ValueError:
             continue
+        g = rec.get("bench_hip_graph")
+        if g is None:                        # summaries before round 6: the tag says it
+            g = "_graph" in os.path.basename(f)
         if kernel in rec.get("kernel", "") and rec.get("algo_bytes_per_launch") == algo_bytes \
-                and rec.get("bench_metric") == metric and rec.get("traffic_bytes_per_launch"):
+                and rec.get("bench_metric") == metric and rec.get("traffic_bytes_per_launch") \
+                and (graph is None or bool(g) == bool(graph)):
             if best is None or os.path.getmtime(f) > os.path.getmtime(best[0]):
                 best = (f, rec)
     return best
@@ -279,6 +283,10 @@ class EncodeWorkload:
         self.W.batch_decode_device(self.dst, so, sl, fps, desc, res)
         body = self.dst[:self.wire_bytes].view(n, fl)[:, self.hl:]
         ok = ok and t.equal(body, self.src.view(n, self.plen))
+        # output hash of the encoded frames, as decoded back (util_amd/dist.py:frame_hash)
+        h = t.zeros(1, dtype=t.int64, device=self.dev)
+        self.W.frame_hash_device(self.dst, desc, res, len(so), fps, h)
+        self.hash = int(h.item()) & 0xFFFFFFFFFFFFFFFF
         return 0 if ok else 1
 
 
@@ -315,12 +323,11 @@ def run_encode(args, dev, world, rank):
                               "ws_enc_tscan_kernel + ws_enc_front_kernel + ws_enc_copy_kernel",
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
-        "cpu_baseline": cpu_encode_baseline(wl, args.cpu_threads or cpu_thread_counts()[-1])
+        "output_hash": "%016x" % D.allreduce_u64([wl.hash], device=dev)[0],
+        "cpu_baseline": cpu_encode_baseline(wl, args.cpu_threads or granted_cpus()[0])
         if rank == 0 and world == 1 and not args.no_cpu else None,
     }
-    if rank == 0:
-        emit(out)
-    return mism
+    return out, mism
 
 
 def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0):
@@ -360,7 +367,9 @@ def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0):
     t1 = timed(1, 1) * threads                     # thread 0 does 1/threads of the frames
     passes = max(2, int(min_seconds / max(1e-6, t1 / threads)))
     tn = timed(threads, passes)
+    g, src = granted_cpus()
     return {"value": round(payload * passes / tn / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "granted_cpus": g, "grant_sources": src,
             "single_thread_gibs": round(payload / t1 / 2**30, 3), "cpu_seconds": round(tn * threads + t1, 2),
             "sample": "%d frames (%.1f MiB payload) of the same workload, %d passes x %d threads, reference "
                       "websocketframeEncode headers + client masking loop (restated)" %
@@ -413,10 +422,18 @@ def run_stream(args, dev, world, rank):
     r = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
     bad = int(wl.verify(expect_plain=(wl.decodes % 2 == 1)) != 0)
     bad += int(int(r["n_frames"]) != wl.nframes or int(r["consumed"]) != wl.wire_bytes or int(r["status"]) != 0)
+    if wl.decodes % 2 == 0:                  # the hash of the decoded (plaintext) stream
+        call()
+        wl.decodes += 1
+    h = torch.zeros(1, dtype=torch.int64, device=dev)
+    W.frame_hash_device(wl.buf, wl.desc, res, 1, wl.nframes, h)
+    ghash = D.allreduce_u64([int(h.item())], device=dev)[0]
     mism = int(D.allreduce([bad], device=dev)[0])
     mean_kern = step_ms / 1e3
+    metric = "WebSocket unmask GiB/s of one raw rx stream (device-resident, device-side frame boundaries)"
+    pmc = pmc_traffic("ws_piece_unmask_kernel", wl.algo_bytes, metric, graph=bool(args.graph))
     out = {
-        "metric": "WebSocket unmask GiB/s of one raw rx stream (device-resident, device-side frame boundaries)",
+        "metric": metric,
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
@@ -427,17 +444,18 @@ def run_stream(args, dev, world, rank):
                    "payload_bytes_per_gpu": wl.payload_bytes},
         "roofline": {"bound": "hbm", "achieved": round(wl.algo_bytes / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
-                     "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_launch": wl.algo_bytes,
+                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
+                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
+                     "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_launch": wl.algo_bytes,
                      "timed": "HIP events at the two ends of the timed region / steps: ws_stream_init_kernel, "
                               "ws_stream_pass_kernel rounds (state on the device), ws_stream_finish_kernel (gated) "
                               "+ ws_piece_unmask_kernel",
                      "kernel_ms_mean": round(step_ms, 4)},
         "verified": mism == 0,
+        "output_hash": "%016x" % ghash,
         "cpu_baseline": None,
     }
-    if rank == 0:
-        emit(out)
-    return mism
+    return out, mism
 
 
 def run_reasm(args, dev, world, rank):
@@ -452,8 +470,12 @@ def run_reasm(args, dev, world, rank):
     msg = torch.empty(wl.nseg * wl.fps * 32, dtype=torch.uint8, device=dev)
     nmsg = torch.empty(wl.nseg, dtype=torch.int32, device=dev)
 
+    rc_max = getattr(args, "readcache", 0) or 0
+    cached = torch.zeros(wl.nseg, dtype=torch.int32, device=dev) if rc_max else None
+
     def step():
-        W.batch_reassemble_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res, out, msg, nmsg)
+        W.batch_reassemble_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res, out, msg, nmsg,
+                                  readcache_max=rc_max, cached=cached)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -465,16 +487,28 @@ def run_reasm(args, dev, world, rank):
     wl.decode()
     t = torch
     plen, hl = wl.plen_h, wl.wirelen_h - wl.plen_h
-    if wl.plen_kind == 0:                    # fixed-size frames: vectorised comparison
+    if wl.plen_kind == 0 and wl.nframes % wl.fps == 0:   # fixed-size frames: every body compared
         n, fl = wl.nframes, int(wl.wirelen_h[0])
         bodies = wl.buf[:wl.wire_bytes].view(n, fl)[:, int(hl[0]):]
-        # output regions start at seg_off; bodies of a segment are back to back
+        # output regions start at seg_off (= s * fps * wire length); bodies of a segment back to back
         seg_body = int(plen[0]) * wl.fps
-        outv = t.stack([out[int(o):int(o) + seg_body] for o in wl.seg_off_h[:64]])
-        bad += int(not t.equal(outv.view(-1, int(plen[0])), bodies[:64 * wl.fps]))
+        outv = out[:wl.wire_bytes].view(wl.nseg, wl.fps * fl)[:, :seg_body]
+        bad += int(not t.equal(outv.reshape(-1), bodies.reshape(-1)))
         nm = nmsg.cpu().numpy()
         bad += int(not (nm == (1 if wl.b0_kind == 2 else wl.fps)).all())
     wl.decode()                              # back to the masked wire
+    # output hash of the delivered messages: util_amd/dist.py:frame_hash over every message
+    # body (len, complete as fin, type 0), through the hash kernel with the message table as
+    # descriptors (message m of segment s in slot s * max_frames + m)
+    m64 = msg.view(t.int64).view(-1, 4)
+    d = t.zeros_like(m64)
+    d[:, 1], d[:, 2], d[:, 3] = m64[:, 0], m64[:, 1], (m64[:, 3] & 0xFFFFFFFF) << 32
+    r = t.zeros(wl.nseg, 2, dtype=t.int64, device=dev)
+    r[:, 1] = nmsg.to(t.int64)
+    h = t.zeros(1, dtype=t.int64, device=dev)
+    W.frame_hash_device(out, d.view(t.uint8).view(-1), r.view(t.uint8).view(-1), wl.nseg, wl.fps, h)
+    ghash = D.allreduce_u64([int(h.item())], device=dev)[0]
+    del d, r, m64
     mism = int(D.allreduce([bad], device=dev)[0])
     mean_kern = float(kern_ms.mean()) / 1e3
     algo = wl.wire_bytes + wl.payload_bytes
@@ -493,6 +527,7 @@ def run_reasm(args, dev, world, rank):
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
         "config": {"workload": "reassemble " + Workload.DESCRIPTION[args.config], "config": args.config,
+                   "readcache_max_size": rc_max,
                    "frames_per_gpu": wl.nframes, "segments_per_gpu": wl.nseg, "wire_bytes_per_gpu": wl.wire_bytes,
                    "payload_bytes_per_gpu": wl.payload_bytes},
         "roofline": {"bound": "hbm", "achieved": round(algo / mean_kern / 1e9, 1), "peak": PEAK_HBM_GBS,
@@ -506,11 +541,10 @@ def run_reasm(args, dev, world, rank):
                          "ws_piece_scan_kernel + ws_reasm_layout_kernel + ws_reasm_gather_kernel"),
                      "kernel_ms_mean": round(mean_kern * 1e3, 4)},
         "verified": mism == 0,
+        "output_hash": "%016x" % ghash,
         "cpu_baseline": cpu,
     }
-    if rank == 0:
-        emit(out_json)
-    return mism
+    return out_json, mism
 
 
 def end_to_end(wl, runs=2):
@@ -563,12 +597,39 @@ def end_to_end(wl, runs=2):
             "pageable": pageable}, runs + 1
 
 
+def granted_cpus():
+    """The CPUs this job may actually use: the affinity mask, capped by the cgroup's CPU quota
+    (v2 cpu.max or v1 cfs_quota/period, rounded up) and by OMP_NUM_THREADS (the GPU box sets it
+    to the job's share, 16, while nproc shows the whole machine). Returns (count, sources)."""
+    import math
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = math.ceil(int(q) / int(p))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0 and p > 0:
+                quota = math.ceil(q / p)
+        except (OSError, ValueError):
+            pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    g = aff
+    if quota:
+        g = min(g, quota)
+    if omp:
+        g = min(g, omp)
+    return max(1, g), {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "omp_num_threads": omp or None}
+
+
 def cpu_thread_counts():
-    """(1, the box's CPU share for this job (OMP_NUM_THREADS, 16 on the GPU box), every CPU
-    this process may run on (sched_getaffinity: nproc)), deduplicated, ascending"""
-    allc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or allc
-    return sorted({1, min(share, allc), allc})
+    """(1, the CPUs granted to this job (granted_cpus: 16 on the GPU box), every CPU of the
+    affinity mask (oversubscribed beyond the grant: a table entry only)), deduplicated, ascending"""
+    g, src = granted_cpus()
+    return sorted({1, g, src["affinity_cpus"]})
 
 
 def cpu_baseline(sample, threads=None, min_seconds=2.0, op="decode", frames_per_segment=16):
@@ -624,8 +685,9 @@ def cpu_baseline(sample, threads=None, min_seconds=2.0, op="decode", frames_per_
             th.join()
         return time.perf_counter() - t0
 
+    granted, src = granted_cpus()
     counts = cpu_thread_counts() if threads is None else sorted({1, threads})
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or counts[-1]
+    share = granted
     rates, wall = {}, 0.0
     for kind, run in runners.items():
         t1 = timed(run, 1, 2)                 # two passes: the buffer returns to its masked state
@@ -644,15 +706,19 @@ def cpu_baseline(sample, threads=None, min_seconds=2.0, op="decode", frames_per_
             wall += tn
             rates[kind][n] = payload * passes / tn / 2**30
     kind = "reference" if "reference" in rates else "port"
-    top = counts[-1]
-    out = {"value": round(rates[kind][top], 3), "unit": "GiB/s", "cores": top, "kind": kind,
+    # value: the best rate on at most the granted CPUs (thread counts above the grant only
+    # contend for the same cores: they stay in the table); cores: the grant
+    within = {n: v for n, v in rates[kind].items() if n <= max(granted, 1)} or rates[kind]
+    best_n = max(within, key=within.get)
+    out = {"value": round(within[best_n], 3), "unit": "GiB/s", "cores": max(n for n in within), "kind": kind,
+           "best_threads": best_n,
            "threads": {str(n): round(v, 3) for n, v in rates[kind].items()},
            "single_thread_gibs": round(rates[kind][1], 3),
-           "cpu_count": os.cpu_count(), "affinity_cpus": counts[-1],
-           "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "granted_cpus": granted, "grant_sources": src, "cpu_count": os.cpu_count(),
            "wall_seconds": round(wall, 2),
-           "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %s; threads %s"
-                     % (nseg * frames_per_segment, nseg, payload / 2**20, what, counts)}
+           "sample": "%d frames (%d rx segments, %.1f MiB payload) of the same workload, %s; threads %s "
+                     "(value: best rate on <= the %d granted CPUs)"
+                     % (nseg * frames_per_segment, nseg, payload / 2**20, what, counts, granted)}
     if kind == "reference" and "port" in rates:
         out["port"] = {"kind": "port", "what": "oracle/ws_oracle.c (the restatement, same flags)",
                        "threads": {str(n): round(v, 3) for n, v in rates["port"].items()}}
@@ -818,6 +884,187 @@ def run_inflight(args, wl0, dev, world, rank):
                     "not part of value", "verified": mism == 0}, mism
 
 
+def run_decode(args, dev, world, rank, wl=None, path=DEFAULT_PATH):
+    """The batch decode (websocketframeBatchDecodeDevice, in place, inputs resident in HBM) of
+    args.config, weak scaling: warm-up, the contract's timed region, the dominant kernel's own
+    launch time in a second region (k2_timing), the generator check and the output hash.
+    Returns (bench line without the extras main() adds, mismatch count of this rank)."""
+    import torch
+    from util_amd import dist as D
+    if wl is None:
+        nfr = args.frames or Workload.CONFIGS[args.config][0]
+        wl = Workload.make(args.config, dev, nframes=args.frames, fps=args.fps, plen=args.plen,
+                           first_frame=rank * nfr)
+    for _ in range(args.warmup):
+        wl.decode()
+    torch.cuda.synchronize()
+    step = wl.decode
+    if args.graph:                    # the call is host-sync free once its workspace exists
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            wl.W.batch_decode_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res)
+
+        def step():
+            graph.replay()
+            wl.decodes += 1
+    elapsed, step_ms = timed_region(step, args.steps, world)
+    elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
+
+    # the dominant kernel's own launch duration, live: the piece path's K2 timed by HIP
+    # events recorded around each K2 launch on the calls' stream (library option
+    # k2_timing), over a second region of the same calls (events between kernels would
+    # perturb the contract's region above, so it is not timed this way)
+    kpath = decode_path(path, wl)
+    k2_ms = None
+    if kpath == 3 and not args.graph:
+        wl.W.set_option("k2_timing", 1)
+        c0, n0 = wl.W.get_stat("k2_calls"), wl.W.get_stat("k2_ns")
+        for _ in range(args.steps):
+            wl.decode()
+        torch.cuda.synchronize()
+        k2_calls, k2_ns = wl.W.get_stat("k2_calls") - c0, wl.W.get_stat("k2_ns") - n0
+        wl.W.set_option("k2_timing", 0)
+        if k2_calls:
+            k2_ms = k2_ns / k2_calls / 1e6
+    # correctness of the timed run: after an odd number of decodes the buffer holds plaintext
+    mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
+    # the output hash of the decoded batch (plaintext state), summed over ranks: the global
+    # stream's frames [0, world * n) (util_amd/dist.py:frame_hash)
+    if wl.decodes % 2 == 0:
+        wl.decode()
+    h = wl.output_hash()
+    mism += wl.verify(expect_plain=True)
+    mism = int(mism)
+    ghash = D.allreduce_u64([h], device=dev)[0]
+
+    value = wl.payload_bytes * world * args.steps / elapsed / 2**30
+    step_kern = step_ms / 1e3
+    mean_kern = k2_ms / 1e3 if k2_ms else step_kern
+    achieved = wl.algo_bytes / step_kern / 1e9                      # the step: the contract's timed region
+    metric = "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames"
+    pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes, metric)
+    timed = ("HIP events at the two ends of the contract's timed region on the calls' stream / steps: " +
+             STEP_KERNELS.get(kpath, KERNELS[kpath]))
+    kernel_timed = ("HIP events recorded around every %s launch on the calls' stream (library "
+                    "option k2_timing), a second region of %d calls" % (KERNELS[kpath], args.steps)) if k2_ms else timed
+    out = {
+        "metric": metric,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
+        "config": {"workload": Workload.DESCRIPTION[args.config], "config": args.config, "hip_graph": args.graph,
+                   "frames_per_gpu": wl.nframes, "frames_per_segment": wl.fps, "segments_per_gpu": wl.nseg,
+                   "wire_bytes_per_gpu": wl.wire_bytes, "payload_bytes_per_gpu": wl.payload_bytes,
+                   "parallelism": "frame-range shards, %d independent GPU(s)" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
+                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
+                     "traffic_kernels": pmc[1].get("kernels_summed") if pmc else None,
+                     "kernel": KERNELS[kpath], "algo_bytes_per_launch": wl.algo_bytes,
+                     "timed": timed,
+                     "step_ms_mean": round(step_kern * 1e3, 4),
+                     "kernel_ms_mean": round(mean_kern * 1e3, 4),
+                     "kernel_frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
+                     "kernel_timed": kernel_timed,
+                     "per_kernel_ns_profiled": pmc[1].get("per_kernel_avg_ns") if pmc else None},
+        "verified": mism == 0,
+        "output_hash": "%016x" % ghash,
+        "cpu_baseline": None,
+    }
+    return out, mism
+
+
+# the single-GPU paths of SURVEY §8 beside the headline (VERDICT r05 "next" 1): name ->
+# (runner, config, graph). Each is timed with the headline's protocol (--steps after
+# --warmup, barrier + synchronize, events at the region's two ends).
+PATHS = {
+    "decode_cfg3": ("decode", "cfg3"),    # websocketframe.c:112-165 under net_reactor.c:515-526, mixed lengths
+    "reasm_cfg5": ("reasm", "cfg5"),      # + net_channel_ex.c:110-157 message delivery, readcache_max_size set
+    "stream_cfg3": ("stream", "cfg3"),    # net_reactor.c:515-526 boundary discovery, one raw stream, eager
+    "encode_cfg2": ("encode", "cfg2"),    # websocketframe.c:167-202 + client masking
+}
+PATH_READCACHE = 1 << 20                  # reasm_cfg5's readcache_max_size: 1 MiB > a 16 KiB message
+
+
+def profile_check(out):
+    """the newest committed rocprofv3 summary of this path (profiles/*_pmc.json, same
+    dominant kernel, algorithmic bytes and metric): its traced step's fraction and this run's
+    fraction over it"""
+    rf = out["roofline"]
+    pmc = pmc_traffic(rf["kernel"], rf["algo_bytes_per_launch"], out["metric"],
+                      graph=bool(out["config"].get("hip_graph")))
+    if not pmc:
+        return None
+    rec = pmc[1]
+    step = rec.get("bench_ms_per_step")
+    kern = rec.get("timed_region_kernel_ms_per_step")
+    res = {"file": os.path.relpath(pmc[0], REPO), "traced_frac": rec.get("bench_frac"),
+           "traced_kernel_ms_per_step": kern,
+           "kernel_trace_frac": round(rf["algo_bytes_per_launch"] / (kern / 1e3) / 1e9 / PEAK_HBM_GBS, 4)
+           if kern else None,
+           "traffic_over_algo": round(rec["traffic_over_algo"], 4) if rec.get("traffic_over_algo") else None,
+           "traced_ms_per_step": step}
+    ref = res["traced_frac"] or res["kernel_trace_frac"]
+    if ref:
+        res["frac_over_traced"] = round(rf["frac"] / ref, 4)
+    return res
+
+
+def run_paths(args, dev):
+    """SURVEY §8's other single-GPU paths, each on its own synthetic batch resident in HBM,
+    timed by the headline's protocol in this same process; every entry verified against the
+    generator / a second decode and hashed (util_amd/dist.py:frame_hash). The raw stream of
+    cfg3 is the same frames as the batch decode of cfg3: their output hashes must be equal."""
+    import copy
+    import torch
+    from util_amd import wsframe as W
+    entries, mism = {}, 0
+    fns = {"decode": run_decode, "reasm": run_reasm, "stream": run_stream, "encode": run_encode}
+    for name, (op, cfg) in PATHS.items():
+        a = copy.copy(args)
+        a.config, a.op, a.graph, a.frames, a.fps, a.plen, a.inflight = cfg, op, False, None, None, None, 1
+        a.readcache = PATH_READCACHE if op == "reasm" else 0
+        t0 = time.perf_counter()
+        if op == "decode":
+            out, m = run_decode(a, dev, 1, 0, path=DEFAULT_PATH)
+        else:
+            out, m = fns[op](a, dev, 1, 0)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        mism += m
+        rf = out["roofline"]
+        e = {"metric": out["metric"], "value": out["value"], "unit": out["unit"],
+             "ms_per_step": out["ms_per_step"], "steps": out["steps"], "warmup": out["warmup"],
+             "verified": out["verified"], "output_hash": out.get("output_hash"),
+             "workload": out["config"]["workload"],
+             "roofline": {"algo_bytes": rf["algo_bytes_per_launch"], "frac": rf["frac"], "kernel": rf["kernel"],
+                          "step_ms_mean": rf.get("step_ms_mean", rf.get("kernel_ms_mean")),
+                          "kernel_frac": rf.get("kernel_frac"), "traffic": rf.get("traffic"),
+                          "timed": rf["timed"]},
+             "profile": profile_check(out), "wall_s": round(time.perf_counter() - t0, 2)}
+        if out.get("cpu_baseline"):
+            e["cpu_baseline"] = out["cpu_baseline"]
+        if op == "reasm":
+            e["readcache_max_size"] = a.readcache
+        entries[name] = e
+    if entries["decode_cfg3"]["output_hash"] != entries["stream_cfg3"]["output_hash"]:
+        mism += 1
+        entries["stream_cfg3"]["verified"] = False
+    entries["stream_cfg3"]["hash_equals_decode_cfg3"] = \
+        entries["decode_cfg3"]["output_hash"] == entries["stream_cfg3"]["output_hash"]
+    W.set_option("k2_timing", 0)
+    return entries, mism
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -891,6 +1138,11 @@ def main():
                     help="CPU baseline threads (0: 1, the job's share (OMP_NUM_THREADS) and every CPU of the process)")
     ap.add_argument("--path", type=int, default=None, help="decode variant (websocketframeGpuSetOption path)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end measurement")
+    ap.add_argument("--no-paths", action="store_true",
+                    help="skip the other single-GPU paths (cfg3 decode, cfg5 reassembly, cfg3 raw stream, cfg2 "
+                         "encode) the default cfg2 run at N = 1 times beside the headline (`paths`)")
+    ap.add_argument("--readcache", type=int, default=0,
+                    help="--op reasm: readcache_max_size (net_channel_ex.c:45-53; 0 = no limit)")
     ap.add_argument("--no-xor-stream", action="store_true", help="skip the plain XOR-stream reference run")
     ap.add_argument("--graph", action="store_true",
                     help="decode: capture one call into a HIP graph and replay it for every step")
@@ -961,7 +1213,10 @@ def main():
     dev = torch.device("cuda", gpu)
     if args.op in ("encode", "reasm", "stream") or (args.op == "decode" and args.config in STRONG):
         fn = {"encode": run_encode, "reasm": run_reasm, "stream": run_stream, "decode": run_strong}[args.op]
-        mism = fn(args, dev, world, rank)
+        out, mism = fn(args, dev, world, rank)
+        out["config"]["alloc"] = args.alloc
+        if rank == 0:
+            emit(out)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(1 if mism else 0)
@@ -998,44 +1253,9 @@ def main():
                               "windows (K2's access pattern without frame logic; websocketframeGpuCalibrate mode 72), "
                               "%d calls timed like the step" % n_c,
                       "ms": round(c_ms, 4), "frac": round(2 * nb / (c_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
-    stream = torch.cuda.current_stream()
-    for _ in range(args.warmup):
-        wl.decode()
-    torch.cuda.synchronize()
-    step = wl.decode
-    if args.graph:                    # the call is host-sync free once its workspace exists
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            wl.W.batch_decode_device(wl.buf, wl.seg_off, wl.seg_len, wl.fps, wl.desc, wl.res)
-
-        def step():
-            graph.replay()
-            wl.decodes += 1
-    elapsed, step_ms = timed_region(step, args.steps, world)
-    kern_ms = np.array([step_ms])
-    from util_amd import dist as D
-    elapsed = D.allreduce([elapsed], op="max", device=dev)[0]      # bench contract: max over ranks
-
-    # the dominant kernel's own launch duration, live: the piece path's K2 timed by HIP
-    # events recorded around each K2 launch on the calls' stream (library option
-    # k2_timing), over a second region of the same calls (events between kernels would
-    # perturb the contract's region above, so it is not timed this way)
-    kpath = decode_path(path, wl)
-    k2_ms = None
-    if kpath == 3 and not args.graph:
-        wl.W.set_option("k2_timing", 1)
-        for _ in range(args.steps):
-            wl.decode()
-        torch.cuda.synchronize()
-        k2_calls, k2_ns = wl.W.get_stat("k2_calls"), wl.W.get_stat("k2_ns")
-        wl.W.set_option("k2_timing", 0)
-        if k2_calls:
-            k2_ms = k2_ns / k2_calls / 1e6
-
+    out, mism = run_decode(args, dev, world, rank, wl=wl, path=path)
     if xor_stream is not None:
-        xor_stream["step_rate_over_xor_stream"] = round(xor_stream["ms"] / step_ms, 4)
-    # correctness of the timed run: after an odd number of decodes the buffer holds plaintext
-    mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
+        xor_stream["step_rate_over_xor_stream"] = round(xor_stream["ms"] / out["roofline"]["step_ms_mean"], 4)
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e, flips = end_to_end(wl)
@@ -1043,68 +1263,12 @@ def main():
         e2e_mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
         e2e["verified"] = e2e_mism == 0
         mism += e2e_mism
-    inflight = None
     if args.inflight > 1:
         inflight, m = run_inflight(args, wl, dev, world, rank)
         mism += m
-    # the output hash of the decoded batch (plaintext state), summed over ranks: the global
-    # stream's frames [0, world * n) (util_amd/dist.py:frame_hash)
-    if wl.decodes % 2 == 0:
-        wl.decode()
-    h = wl.output_hash()
-    mism += wl.verify(expect_plain=True)
-    mism, = D.allreduce([mism], device=dev)
-    mism = int(mism)
-    ghash = D.allreduce_u64([h], device=dev)[0]
-
-    payload_all = wl.payload_bytes * world * args.steps
-    value = payload_all / elapsed / 2**30
-    step_kern = float(kern_ms.mean()) / 1e3
-    mean_kern = k2_ms / 1e3 if k2_ms else step_kern
-    achieved = wl.algo_bytes / step_kern / 1e9                      # the step: the contract's timed region
-    metric = "WebSocket unmask GiB/s (device-resident) + %HBM peak, 1M x 4KiB frames"
-    pmc = pmc_traffic(KERNELS[kpath], wl.algo_bytes, metric)
-    timed = ("HIP events at the two ends of the contract's timed region on the calls' stream / steps: " +
-             STEP_KERNELS.get(kpath, KERNELS[kpath]))
-    kernel_timed = ("HIP events recorded around every %s launch on the calls' stream (library "
-                    "option k2_timing), a second region of %d calls" % (KERNELS[kpath], args.steps)) if k2_ms else timed
-    out = {
-        "metric": metric,
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, generated in HBM)",
-        "config": {"workload": Workload.DESCRIPTION[args.config], "config": args.config, "hip_graph": args.graph,
-                   "frames_per_gpu": wl.nframes, "frames_per_segment": wl.fps, "segments_per_gpu": wl.nseg,
-                   "wire_bytes_per_gpu": wl.wire_bytes, "payload_bytes_per_gpu": wl.payload_bytes,
-                   "parallelism": "frame-range shards, %d independent GPU(s)" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4),
-                     "traffic": int(pmc[1]["traffic_bytes_per_launch"]) if pmc else None,
-                     "traffic_source": os.path.relpath(pmc[0], REPO) if pmc else None,
-                     "traffic_kernels": pmc[1].get("kernels_summed") if pmc else None,
-                     "kernel": KERNELS[kpath], "algo_bytes_per_launch": wl.algo_bytes,
-                     "timed": timed,
-                     "step_ms_mean": round(step_kern * 1e3, 4),
-                     "kernel_ms_mean": round(mean_kern * 1e3, 4),
-                     "kernel_frac": round(wl.algo_bytes / mean_kern / 1e9 / PEAK_HBM_GBS, 4),
-                     "kernel_timed": kernel_timed,
-                     "per_kernel_ns_profiled": pmc[1].get("per_kernel_avg_ns") if pmc else None},
-        "verified": mism == 0,
-        "output_hash": "%016x" % ghash,
-        "cpu_baseline": None,
-        "xor_stream": xor_stream,
-        "e2e": e2e,
-    }
-    if inflight is not None:
         out["inflight"] = inflight
+    out["xor_stream"] = xor_stream
+    out["e2e"] = e2e
     if sample is not None:
         out["cpu_baseline"] = cpu_baseline(sample, args.cpu_threads or None)
     if args.scatter and world > 1:                                 # SURVEY §8e (1), outside the timed region
@@ -1116,6 +1280,16 @@ def main():
                           "GBps_per_link": round(wl.wire_bytes / dt / 1e9, 1),
                           "GBps_total": round((world - 1) * wl.wire_bytes / dt / 1e9, 1)}
         del recv
+    # every other single-GPU path of SURVEY §8, timed by the same protocol in the same run
+    # (N = 1 only: the scaling points time the headline alone)
+    if world == 1 and not args.no_paths and args.config == "cfg2" and args.frames is None:
+        wl.free()
+        del wl
+        out["paths"], m = run_paths(args, dev)
+        mism += m
+    mism = int(D.allreduce([mism], device=dev)[0])
+    out["verified"] = out["verified"] and mism == 0
+    out["config"]["alloc"] = args.alloc
     if rank == 0:
         emit(out)
     if world > 1:

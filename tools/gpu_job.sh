@@ -42,7 +42,7 @@ case $mode in
         label=${arm%%|*}; spec=${arm#*|}
         envs=""; args=$spec
         if [[ $spec == *" -- "* ]]; then envs=${spec%% -- *}; args=${spec#* -- }; fi
-        env $envs timeout -k 10 400 python bench.py $args --no-cpu --no-e2e --no-xor-stream \
+        env $envs timeout -k 10 400 python bench.py $args --no-cpu --no-e2e --no-xor-stream --no-paths \
           > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err || { echo "FAIL $label"; tail -5 gpurun_out/ab_one.err; exit 1; }
         python - "$label" "$args" >> gpurun_out/ab_${T}.log <<'EOF'
 import json, sys

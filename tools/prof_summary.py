@@ -15,8 +15,21 @@ untraced run with the CPU baseline and end-to-end fields).
 
 HBM traffic per launch (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are
 in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
-streaming read, so traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+streaming read (the guide's ×2), so a STREAMING kernel's traffic = (2 * FETCH_SIZE +
+WRITE_SIZE) * 1024. The ×2 applies to that access pattern only: the walk kernels (K1's
+16-lane scattered 32-B header reads, the raw stream's candidate / owner / emit walks, the
+encode front's random edge windows) fetch about one 64-B line per request and are
+reported raw, FETCH_SIZE * 1024 (cfg2 K1: 76.7 MB raw ≈ one 64-B line per 4 KiB frame).
 """
+
+# kernels whose reads are wide coalesced streams (16 B per lane over whole pieces / segments):
+# the only ones FETCH_SIZE is doubled for
+STREAMING = ("ws_piece_unmask_kernel", "ws_enc_copy_kernel", "ws_segfuse_kernel", "ws_reasm_seg_kernel",
+             "ws_reasm_gather_kernel", "ws_walker_kernel")
+
+
+def fetch_factor(kernel):
+    return 2.0 if any(kernel.startswith(k) or k in kernel for k in STREAMING) else 1.0
 import csv
 import json
 import os
@@ -58,7 +71,7 @@ def main():
     rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     stats = [r for r in rows if kernel in r["Name"]]
     per_kernel = {}
-    fetch_kib = write_kib = 0.0
+    fetch_kib = write_kib = fetch_corr = 0.0
     nf = nw = 0
     for k in names:
         st = [r for r in rows if k in r["Name"]]
@@ -67,12 +80,14 @@ def main():
         f, a = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), k, "FETCH_SIZE")
         w, b = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), k, "WRITE_SIZE")
         per_kernel[k] = {"avg_ns": float(st[0]["AverageNs"]) if st else None, "calls": int(st[0]["Calls"]) if st else 0,
-                         "fetch_kib": f, "write_kib": w}
+                         "fetch_kib": f, "write_kib": w, "fetch_factor": fetch_factor(k)}
         if f is None or w is None:
             fetch_kib = write_kib = None
+            fetch_corr = None
         elif fetch_kib is not None:
             fetch_kib += f
             write_kib += w
+            fetch_corr += fetch_factor(k) * f
         if k == kernel:
             nf, nw = a, b
     bench = json.load(open(os.path.join(src, "bench.json")))
@@ -90,14 +105,19 @@ def main():
         "per_kernel_avg_ns": {k: v["avg_ns"] for k, v in per_kernel.items()},
         "fetch_size_kib_per_launch": fetch_kib, "fetch_dispatches": nf,
         "write_size_kib_per_launch": write_kib, "write_dispatches": nw,
-        "fetch_bytes_corrected": 2 * fetch_kib * 1024 if fetch_kib is not None else None,
+        "fetch_bytes_corrected": fetch_corr * 1024 if fetch_kib is not None else None,
         "write_bytes": write_kib * 1024 if write_kib is not None else None,
         "algo_bytes_per_launch": algo,
         "bench_metric": bench.get("metric"),
-        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB -> bytes",
+        "bench_frac": rf.get("frac"),
+        "bench_hip_graph": bool(bench.get("config", {}).get("hip_graph")),
+        "bench_config": bench.get("config"),
+        "correction": "FETCH_SIZE x2 for the streaming kernels only (%s: gfx950 reports half of wide coalesced "
+                      "streaming reads), x1 for walk kernels (scattered line requests), KiB -> bytes"
+                      % ", ".join(k for k in names if fetch_factor(k) == 2.0),
     }
     if fetch_kib is not None and write_kib is not None:
-        rec["traffic_bytes_per_launch"] = (2 * fetch_kib + write_kib) * 1024
+        rec["traffic_bytes_per_launch"] = (fetch_corr + write_kib) * 1024
         rec["traffic_over_algo"] = rec["traffic_bytes_per_launch"] / algo
     if "traffic_bytes_per_launch" in rec:
         # the bench line ran before this profile's counter passes: its traffic field is filled
