@@ -225,7 +225,12 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:
  * chunk-parallel walk 1 linked on the device, 2 eager calls linked by the host, 0 one wavefront;
  * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
- * call's chunk records linked in parallel 0/1), "k2_timing" (see
+ * call's chunk records linked in parallel 0/1), "stream_split" / "stream_split_wait" /
+ * "stream_c0" / "stream_side_prio" (raw stream, device-planned walk: the unmask's first launch takes this many 256ths
+ * of the pieces, 0..255, 0 = one launch, while the walk of the stream past them runs beside it;
+ * that walk starts after the plan 0, after the first part's owner walks 1 or its emit 2; the first
+ * part's chunks are the usual chunk >> 0..6; "stream_side_prio": the side stream's priority, 0
+ * default, 1 least, 2 greatest), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);
@@ -235,7 +240,8 @@ WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long va
  * (chunks of a long stream written from the chunk-parallel walk's records),
  * "stream_rw_chunk_walks" (chunks it had to walk with one wavefront), "stream_skips" (eager raw-stream
  * calls since load that skipped the pass rounds because the previous chunk walk on the stream saw
- * lengths that keep changing), "capture_adoptions" (graph captures since load that took over the
+ * lengths that keep changing), "stream_splits" (raw-stream calls since load whose unmask
+ * ran as two launches beside the split walk, option "stream_split"), "capture_adoptions" (graph captures since load that took over the
  * workspace slot of a destroyed graph whose replays had all finished); with the option
  * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece
  * path's unmask launches since the option was set, from HIP events around each launch;

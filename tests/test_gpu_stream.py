@@ -437,3 +437,96 @@ def test_two_raw_streams_in_parallel_threads(dev):
         t.join(timeout=100)
     assert not any(t.is_alive() for t in ts), "a decode thread hung"
     assert not errors, errors
+
+
+# --- round 6: the split walk (option "stream_split"): K2 as two launches, the walk of the stream
+# past the first launch's pieces on a side stream beside it (ws_stream.hip RwSplit) -------------
+
+@pytest.fixture
+def split_opts():
+    """restores the split options after a test that changes them"""
+    yield
+    W.set_option("stream_split", 16)
+    W.set_option("stream_split_wait", 0)
+    W.set_option("stream_c0", 2)
+    W.set_option("stream_rw", 1)
+
+
+def _frames_before(wire, nbytes, mf=1 << 17):
+    od, orr = oracle_segments(wire.copy(), [0], [len(wire)], mf)
+    fo = od["frame_off"][:int(orr[0]["n_frames"])]
+    return int(np.searchsorted(fo, nbytes))
+
+
+@pytest.mark.parametrize("split,wait,c0", [(1, 0, 2), (16, 0, 2), (16, 1, 0), (16, 2, 6), (40, 0, 3), (128, 0, 2),
+                                           (255, 2, 2)])
+def test_stream_split_boundaries(dev, split_opts, split, wait, c0):
+    """the split point (piece p0 = npieces * split / 256) falls inside a frame; part 0 (small chunks)
+    hands the chain over to part 1 mid-frame; streams ending (max_frames, truncation, garbage, a
+    decode error) inside part 0, at the hand-off and inside part 1; two buffer phases. Every call
+    bit-exact vs the oracle and the split taken (stat stream_splits)"""
+    W.set_option("stream_split", split)
+    W.set_option("stream_split_wait", wait)
+    W.set_option("stream_c0", c0)
+    rng = np.random.default_rng(600 + split)
+    wire = long_stream(rng, 40 << 20, mix3)
+    x = len(wire) * split // 256
+    n0 = W.get_stat("stream_splits")
+    run(dev, wire, 1 << 16)
+    run(dev, wire, 1 << 16, shift=7)
+    assert W.get_stat("stream_splits") >= n0 + 2
+    # max_frames inside part 0, just past the split point and inside part 1
+    for at in (x // 2, x + 70000, (x + len(wire)) // 2):
+        mf = max(1, _frames_before(wire, at))
+        r = run(dev, wire, mf)
+        assert int(r["n_frames"]) <= mf
+    # garbage and a LEN_WRAP header around the split point
+    for at in (max(0, x - 5000), x + 3, min(len(wire) - 64, x + (20 << 20) // 3)):
+        g = wire.copy()
+        g[at:at + 37] = rng.integers(0, 256, 37, dtype=np.uint8)
+        run(dev, g, 1 << 16)
+    run(dev, wire[:x + 1000].copy(), 1 << 16)                                     # truncated after the split
+    run(dev, wire[:len(wire) - 999].copy(), 1 << 16)
+
+
+def test_stream_split_long_frames_and_host_path(dev, split_opts):
+    """frames longer than part 0's small chunks (its owner walks cross them; entries outside the
+    windows: the serial linker of a part) and the eager host-linked path (stream_rw 2: no split)"""
+    W.set_option("stream_split", 64)
+    W.set_option("stream_c0", 6)
+    wire = long_stream(np.random.default_rng(611), 40 << 20, lambda g: g.integers(100 << 10, 1 << 20))
+    run(dev, wire, 1 << 12)
+    wire2 = long_stream(np.random.default_rng(612), 24 << 20, mix3)
+    W.set_option("stream_rw", 2)
+    run(dev, wire2, 1 << 16)
+
+
+def test_stream_split_captured(dev, split_opts):
+    """a captured raw-stream decode with the split (the side stream forks and joins inside the
+    graph): replays of changing bytes, a max_frames stop in part 0, bit-exact each time"""
+    W.set_option("stream_split", 32)
+    rng = np.random.default_rng(621)
+    wire = long_stream(rng, 32 << 20, mix3)
+    cw = _cut_stream("garbage", rng, wire, keep_len=True)
+    n = len(wire)
+    for mf in (1 << 16, max(1, _frames_before(wire, n * 32 // 256 // 2))):
+        d = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+        desc = torch.zeros(mf * 32, dtype=torch.uint8, device=dev)
+        res = torch.zeros(16, dtype=torch.uint8, device=dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            W.stream_decode_device(d, n, mf, desc, res)
+        for w in (wire, cw, wire, wire):
+            ob = w.copy()
+            od, orr = oracle_segments(ob, [0], [n], mf)
+            d[:n].copy_(torch.from_numpy(w).to(dev))
+            desc.zero_()
+            res.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            gr = res.cpu().numpy().view(W.SEGRES_DTYPE)[0]
+            assert tuple(gr) == tuple(orr[0]), (mf, gr, orr[0])
+            assert np.array_equal(desc.cpu().numpy().view(W.DESC_DTYPE)[:int(gr["n_frames"])],
+                                  od[:int(orr[0]["n_frames"])])
+            assert np.array_equal(d[:n].cpu().numpy(), ob)
+        del g

@@ -33,8 +33,10 @@ extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
+extern WsOpt ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio;
 size_t ws_workspace_bytes_total();
-extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips;
+extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips,
+    ws_stat_stream_splits;
 extern std::atomic<unsigned long long> ws_stat_adoptions;
 
 int ws_set_err(const char* what, hipError_t e) {
@@ -101,6 +103,22 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         if (value < 0 || value > 1) return -1;
         ws_stream_plink = (int)value;
     }
+    else if (!strcmp(name, "stream_split")) {
+        if (value < 0 || value > 255) return -1;
+        ws_stream_split = (int)value;
+    }
+    else if (!strcmp(name, "stream_split_wait")) {
+        if (value < 0 || value > 2) return -1;
+        ws_stream_split_wait = (int)value;
+    }
+    else if (!strcmp(name, "stream_side_prio")) {
+        if (value < 0 || value > 2) return -1;
+        ws_stream_side_prio = (int)value;
+    }
+    else if (!strcmp(name, "stream_c0")) {
+        if (value < 0 || value > 6) return -1;
+        ws_stream_c0 = (int)value;
+    }
     else if (!strcmp(name, "stream_rounds")) {
         if (value < 1 || value > 64) return -1;
         ws_stream_rounds = (int)value;
@@ -128,6 +146,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     if (!strcmp(name, "stream_rw_chunks")) *value = ws_stat_rw_chunks.load();
     else if (!strcmp(name, "stream_rw_chunk_walks")) *value = ws_stat_rw_chunk_walks.load();
     else if (!strcmp(name, "stream_skips")) *value = ws_stat_stream_skips.load();
+    else if (!strcmp(name, "stream_splits")) *value = ws_stat_stream_splits.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
     else if (!strcmp(name, "capture_adoptions")) *value = ws_stat_adoptions.load();
 
@@ -168,6 +187,9 @@ struct WsStreamWs {
     std::vector<std::pair<void*, size_t>> retired;   // buffers replaced while capturing (the graph still uses them)
     hipEvent_t done = nullptr;     // captured slots: recorded at the end of every captured call (an event
                                    // record node), so a destroyed graph's replays are known to be finished
+    hipStream_t side = nullptr;    // the raw stream's split walk: part 1 runs here (ws_stream.hip RwSplit)
+    int side_prio = 0;             // ... created with this priority choice (0 default, 1 least, 2 greatest)
+    hipEvent_t sev[3] = {};        // ... and its fork / join events
 };
 struct WsDevState {
     int init = 0;
@@ -491,6 +513,38 @@ int WsSlot::aux(size_t dbytes, size_t hbytes, WsAux* out) {
     out->h = w->hws;
     out->h_dev = w->hws_dev;
     out->state_ok = &w->aux_state_ok;
+    return 0;
+}
+
+// the side stream and events of the raw stream's split walk (created once per slot, outside any
+// capture's rules: relaxed mode; a capture forks into the side stream through its events)
+int WsSlot::side(hipStream_t* side_out, hipEvent_t* ev, int prio) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (w->side && w->side_prio != prio && !capturing(st)) {      // another priority asked for (eager calls only)
+        hipError_t e = hipStreamSynchronize(w->side);
+        if (e == hipSuccess) e = hipStreamDestroy(w->side);
+        if (e != hipSuccess) return ws_set_err("side stream (raw stream split)", e);
+        w->side = nullptr;
+    }
+    if (!w->side || !w->sev[2]) {
+        hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&m);
+        int least = 0, greatest = 0;
+        hipError_t e = hipSuccess;
+        if (!w->side) {
+            if (prio) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+            if (e == hipSuccess)
+                e = prio ? hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, prio == 1 ? least : greatest)
+                         : hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+            w->side_prio = prio;
+        }
+        for (int k = 0; k < 3 && e == hipSuccess; ++k)
+            if (!w->sev[k]) e = hipEventCreateWithFlags(&w->sev[k], hipEventDisableTiming);
+        (void)hipThreadExchangeStreamCaptureMode(&m);
+        if (e != hipSuccess) return ws_set_err("side stream (raw stream split)", e);
+    }
+    *side_out = w->side;
+    for (int k = 0; k < 3; ++k) ev[k] = w->sev[k];
     return 0;
 }
 

@@ -429,6 +429,7 @@ struct WsSlot {
     int encode_workspace(size_t bytes, void** out);
     int aux(size_t dbytes, size_t hbytes, WsAux* out);
     int advice(int** host, int** dev);                             // the stride hint words (eager)
+    int side(hipStream_t* side, hipEvent_t* ev, int prio);         // the raw stream's split walk: side stream + 3 events
 };
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,

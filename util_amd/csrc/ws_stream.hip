@@ -162,6 +162,7 @@ struct SwOut {            // where a stream_walk stopped: the next frame, its in
     u32 nf, ended;
     u32 steps;            // header rounds the walk took (a run of equal frames takes one per 64)
     u32 maxlen;           // the longest frame it took (wire bytes; only when asked: want_max)
+    u32 cnt;              // the item count a finishing walk writes (frames + an unconsumed ret == 0 frame)
 };
 __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ buf, u64 len, u64 P0, u64 g0, u32 nf0,
                                             u64 end, bool last, u32 max_frames, WebsocketFrameDesc_t* __restrict__ desc,
@@ -253,6 +254,7 @@ __device__ __forceinline__ SwOut stream_walk(const unsigned char* __restrict__ b
     r.ended = at_bnd ? 0u : 1u;
     r.steps = steps;
     r.maxlen = 0;
+    r.cnt = nf + extra;
     if (want_max) {
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
@@ -505,15 +507,51 @@ struct RwOwn {            // phase B: the walk from a window exit to the chunk's
 };
 
 // The walk's geometry chosen on the device (captured calls: the host cannot read the sample):
-// R1-R3, the linker and the emit take it from here; scratch is sized for the caps at capture
-struct RwPlan {
-    u64 P;                // the chunk grid's origin (the entry after the sample)
-    u64 C;                // chunk bytes
-    u32 H, nchunks, capc, stgn;
-    u32 need_mask, active, nf, nrows;
-    u64 sample_out[4];    // stream_walk's report of the sample / of a linked chunk walk
-    u32 seen_max, pad0;   // the longest frame the previous walk on this stream wrote (emit, linker)
+// R1-R3, the linker and the emit take it from here; scratch is sized for the caps at capture.
+// Round 6: the rest of the stream after the sample is one or two PARTS, each a chunk grid of
+// its own. With a split (stream_split), part 0 = [P, Pb) in small chunks (its owner walks are
+// short: it is the walk K2's first launch waits for) and part 1 = [Pb, len) in the usual
+// chunks; part 1's walk runs on a side stream beside K2 over part 0's pieces. Chunk arrays are
+// indexed by the global chunk g = cbase + local index; per-part lists start at their bases.
+struct RwPart {
+    u64 P;                // the part's chunk grid origin
+    u64 C;                // its chunk bytes
+    u32 H, n, cbase, capc; // window bytes, chunks, first global chunk, candidates per chunk
+    u32 stgn, pad;        // staging per owner
+    u64 stg_base, cand_base;  // where its staging and candidate lists start (entries)
 };
+struct RwPlan {
+    RwPart pt[2];         // part 1 empty (n = 0) without a split
+    u32 nchunks;          // n0 + n1 (global chunk count)
+    u32 need_mask, active, nf;   // nf: frames before pt[0].P
+    u32 nrows[2], linked[2];     // emit rows of each part (rows at tab[cbase + r]); linked: rows final
+    u64 sample_out[4];    // stream_walk's report of the sample / of a linked chunk walk
+    u32 seen_max;         // the longest frame the previous walk on this stream wrote (emit, linker)
+    u32 nw0;              // the item count K2's first launch reads: every item it may need is written
+    u64 h_ent;            // the hand-off from part 0 to part 1: the chain's entry, frames before it,
+    u32 h_nf, h_state;    // state 0 none yet, 1 part 1 continues at h_ent, 2 the walk ended in part 0
+};
+static_assert(sizeof(RwPlan) <= 256, "RwPlan lies in the zeroed aux range (WS_AUX_ZERO)");
+
+// a kernel's chunk grid: the plan's part (device-planned calls) or the host's arguments
+struct RwGeo {
+    u64 P, C;
+    u32 H, n, cbase, capc, stgn, nall, need_mask;
+    u64 stg_base, cand_base;
+};
+__device__ __forceinline__ RwGeo rw_geo(const RwPlan* plan, int part, u64 P, u64 C, u32 H, u32 nchunks, u32 capc,
+                                        u32 stgn, u32 need_mask) {
+    RwGeo G;
+    if (plan) {
+        const RwPart& t = plan->pt[part];
+        G.P = t.P; G.C = t.C; G.H = t.H; G.n = t.n; G.cbase = t.cbase; G.capc = t.capc; G.stgn = t.stgn;
+        G.nall = plan->nchunks; G.need_mask = plan->need_mask; G.stg_base = t.stg_base; G.cand_base = t.cand_base;
+    } else {
+        G.P = P; G.C = C; G.H = H; G.n = nchunks; G.cbase = 0; G.capc = capc; G.stgn = stgn; G.nall = nchunks;
+        G.need_mask = need_mask; G.stg_base = 0; G.cand_base = 0;
+    }
+    return G;
+}
 
 // a wavefront's longest frame -> the plan's seen_max (the next call's windows cover it)
 __device__ __forceinline__ void rw_note_max(const RwPlan* plan, u32 mx, u32 lane) {
@@ -558,20 +596,19 @@ __device__ __forceinline__ u32 rw_step(uintptr_t origin, u64 len, u64& pos, bool
 __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __restrict__ buf, u64 len, u64 P,
                                                          u64 C, u32 H, u32 nchunks, u32 need_mask,
                                                          u64* __restrict__ cand, u32* __restrict__ nrec, u32 capc,
-                                                         const RwPlan* __restrict__ plan) {
-    if (plan) {                                                              // geometry from the device
-        if (!plan->active) return;
-        P = plan->P; C = plan->C; H = plan->H; nchunks = plan->nchunks; need_mask = plan->need_mask;
-        capc = plan->capc;
-    }
+                                                         const RwPlan* __restrict__ plan, int part) {
+    if (plan && !plan->active) return;
+    const RwGeo G = rw_geo(plan, part, P, C, H, nchunks, capc, 0, need_mask);   // geometry from the device
+    P = G.P; C = G.C; H = G.H; need_mask = G.need_mask; capc = G.capc;
     const u32 lane = threadIdx.x & 63;
     __shared__ unsigned short s_cand[256 / 64][RW_WCAP];                     // a wave's candidates (position in its 4 KiB)
     const u32 per = H / RW_TPOS;                                             // a multiple of 64: one
     // grid-stride (a captured call's grid is sized for the largest geometry); a whole
     // wavefront takes the same iterations
     for (u64 t = (u64)blockIdx.x * 256 + threadIdx.x;; t += (u64)gridDim.x * 256) {
-    const u64 c = t / per;                                                   // chunk per wavefront
-    if (c >= nchunks) return;
+    const u64 c = t / per;                                                   // chunk per wavefront (local)
+    if (c >= G.n) return;
+    const u64 gc = G.cbase + c;                                              // ... global
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
     const u64 cs0 = P + c * C;
     const uintptr_t a = ((origin + cs0) & ~(uintptr_t)15) + (t % per) * RW_TPOS;
@@ -631,7 +668,7 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const u64 pw0 = (a - origin) - (u64)lane * RW_TPOS;                      // lane 0's first position
     const u64 cend = cs0 + C;
-    u64* cl = cand + c * capc;
+    u64* cl = cand + G.cand_base + c * capc;
     const u32 staged = total < RW_WCAP ? total : RW_WCAP;
     // one verdict per lane per pass: survivors appended to the chunk's list (one atomic per pass)
     auto verdict = [&](bool have, u64 pos0) {
@@ -644,7 +681,7 @@ __global__ __launch_bounds__(256) void ws_rw_cand_kernel(const unsigned char* __
         const u64 km = __ballot(keep);
         const u32 cnt = (u32)__builtin_popcountll(km);
         u32 ob = 0;
-        if (lane == 0 && cnt) ob = atomicAdd(nrec + 4 * c + 2, cnt);         // the chunk's counter
+        if (lane == 0 && cnt) ob = atomicAdd(nrec + 4 * gc + 2, cnt);        // the chunk's counter
         ob = (u32)__shfl((int)ob, 0);
         if (keep) {
             const u32 o = ob + (u32)__builtin_popcountll(km & ((1ull << lane) - 1));
@@ -675,19 +712,18 @@ __global__ __launch_bounds__(256) void ws_rw_spec_kernel(const unsigned char* __
                                                          const u64* __restrict__ cand, u32 capc,
                                                          RwRec* __restrict__ recs, u32* __restrict__ nrec,
                                                          unsigned long long* __restrict__ dx,
-                                                         const RwPlan* __restrict__ plan) {
-    if (plan) {
-        if (!plan->active) return;
-        P = plan->P; C = plan->C; H = plan->H; nchunks = plan->nchunks; need_mask = plan->need_mask;
-        capc = plan->capc;
-    }
+                                                         const RwPlan* __restrict__ plan, int part) {
+    if (plan && !plan->active) return;
+    const RwGeo G = rw_geo(plan, part, P, C, H, nchunks, capc, 0, need_mask);
+    P = G.P; C = G.C; H = G.H; need_mask = G.need_mask; capc = G.capc;
+    nchunks = G.nall;                                                        // (the last chunk's pool)
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
-    const u64 n = (u64)nchunks * capc;
+    const u64 n = (u64)G.n * capc;
     for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += (u64)gridDim.x * 256) {
-        const u64 c = i / capc;
-        if (i - c * capc >= nrec[4 * c + 2]) continue;                      // past the chunk's candidates
-        const u64 start = cand[i];
-        const u64 cs0 = P + c * C, cend = cs0 + C, wend = cs0 + H;
+        const u64 cl = i / capc, c = G.cbase + cl;                           // local, global chunk
+        if (i - cl * capc >= nrec[4 * c + 2]) continue;                     // past the chunk's candidates
+        const u64 start = cand[G.cand_base + i];
+        const u64 cs0 = P + cl * C, cend = cs0 + C, wend = cs0 + H;
         u64 pos = start;
         u32 cnt = 0, r = 0;
         while (pos < wend && (r = rw_step(origin, len, pos, need_mask)) == 0) ++cnt;
@@ -728,18 +764,18 @@ __global__ __launch_bounds__(RW_OWN_T) void ws_rw_own_kernel(const unsigned char
                                                         u32 nchunks, u32 need_mask,
                                                         const unsigned long long* __restrict__ dx,
                                                         RwOwn* __restrict__ own, u32* __restrict__ stg, u32 stgn,
-                                                        const RwPlan* __restrict__ plan) {
-    if (plan) {
-        if (!plan->active) return;
-        P = plan->P; C = plan->C; nchunks = plan->nchunks; need_mask = plan->need_mask; stgn = plan->stgn;
-    }
-    const u64 oi = (u64)blockIdx.x * RW_OWN_T + threadIdx.x;
-    if (oi >= (u64)nchunks * RW_D) return;
+                                                        const RwPlan* __restrict__ plan, int part) {
+    if (plan && !plan->active) return;
+    const RwGeo G = rw_geo(plan, part, P, C, 0, nchunks, 0, stgn, need_mask);
+    P = G.P; C = G.C; need_mask = G.need_mask; stgn = G.stgn;
+    const u64 ol = (u64)blockIdx.x * RW_OWN_T + threadIdx.x;                 // local owner index
+    if (ol >= (u64)G.n * RW_D) return;
+    const u64 oi = (u64)G.cbase * RW_D + ol;                                 // global
     u64 pos = dx[oi];
     if (!pos) return;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
-    const u64 c = oi / RW_D, cs0 = P + c * C, cend = cs0 + C;
-    u32* sl = stg + oi * stgn;
+    const u64 c = ol / RW_D, cs0 = P + c * C, cend = cs0 + C;
+    u32* sl = stg + G.stg_base + ol * stgn;
     u32 nb = 0, r = 0;
     u64 over = 0;
     while (pos < cend) {
@@ -769,26 +805,36 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
-                                                        const RwPlan* __restrict__ plan) {
+                                                        RwPlan* __restrict__ plan, int part) {
+    u64 row = blockIdx.x, obase = 0, sbase = 0;
     if (plan) {                                                              // rows written by the linker
-        if (!plan->active || blockIdx.x >= plan->nrows) return;
-        stgn = plan->stgn;
+        if (!plan->active || blockIdx.x >= plan->nrows[part] || (part == 1 && plan->h_state != 1)) return;
+        const RwPart& pt = plan->pt[part];
+        stgn = pt.stgn;
+        row += pt.cbase;                                                     // the part's rows start at its first chunk
+        obase = (u64)pt.cbase * RW_D;
+        sbase = pt.stg_base;
     }
-    const u64* t = tab + 8 * blockIdx.x;
+    const u64* t = tab + 8 * row;
     const u64 ent = t[0], exit_w = t[1], nf0 = t[2], cnt_w = t[3], oi = t[4], n_par = t[5], cs0 = t[7];
     const bool last = t[6] != 0;
     const u32 lane = threadIdx.x;
+    // the row that ends the walk in part 0 also writes the count K2's first launch reads
+    auto note_end = [&](const SwOut& o) {
+        if (plan && part == 0 && last && lane == 0) plan->nw0 = o.cnt;
+    };
     if (oi == ~0ull) {
         const SwOut o = stream_walk(buf, len, ent, 0, (u32)nf0, len, true, max_frames, desc, items, ptr, pend, nwork,
                                     res, lane, nullptr, plan != nullptr);
         rw_note_max(plan, o.maxlen, lane);
+        note_end(o);
         return;
     }
     const SwOut o1 = stream_walk(buf, len, ent, 0, (u32)nf0, exit_w, false, max_frames, desc, items, ptr, pend, nwork,
                                  res, lane, nullptr, plan != nullptr);
     u32 mx = o1.maxlen;
     const RwOwn ow = own[oi];
-    const u32* sl = stg + oi * stgn;
+    const u32* sl = stg + sbase + (oi - obase) * stgn;
     const u64 lead0 = reinterpret_cast<uintptr_t>(buf) & 15;
     const uintptr_t origin = reinterpret_cast<uintptr_t>(buf);
     for (u64 i = lane; i < n_par; i += 64) {
@@ -816,6 +862,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
     const SwOut o2 = stream_walk(buf, len, next, 0, (u32)(nf0 + cnt_w + n_par), last ? len : ow.exit, last, max_frames,
                                  desc, items, ptr, pend, nwork, res, lane, nullptr, plan != nullptr);
     rw_note_max(plan, o2.maxlen > mx ? o2.maxlen : mx, lane);
+    note_end(o2);
 }
 
 // ---- the chunk-parallel walk inside a captured call (no host reads): the plan kernel
@@ -831,14 +878,22 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
-                                                        SdMirror* __restrict__ mirror) {
+                                                        SdMirror* __restrict__ mirror, u64 split_x, u32 c0_shift) {
     const u32 lane = threadIdx.x;
     const u32 seen = plan->seen_max;        // the previous walk's longest frame (0 before the first: WS_AUX_ZERO)
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
     const int dev = fresh == 2;
     if (dev) fresh = sd->walk_hint != 0;
+    // the walk is finished before any part: K2's first launch reads the final count
+    auto finished = [&](u32 cnt) {
+        if (lane == 0) {
+            plan->active = 0;
+            plan->nw0 = cnt;
+            plan->h_state = 2;
+        }
+    };
     if (!fresh && sd->phase == SD_DONE) {                                    // the passes finished it
-        if (lane == 0) plan->active = 0;
+        finished(nwork[0]);
         return;
     }
     // fresh: no pass rounds ran (the previous chunk walk on this stream saw lengths that keep
@@ -866,35 +921,69 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
         if (dev) sd->walk_hint = hint;                                       // read by the next replay
     }
     if (o.ended) {
-        if (lane == 0) plan->active = 0;
+        finished(o.cnt);
         return;
     }
     const u64 P1 = o.next;
     const u64 mean = o.nf > nf ? (P1 - P) / (o.nf - nf) : (P1 - P);
     if ((len - P1) / (mean ? mean : 1) < RW_MIN_FRAMES) {                   // a short rest: this wavefront
-        stream_walk(buf, len, P1, 0, o.nf, len, true, max_frames, desc, items, ptr, pend, nwork, res, lane);
-        if (lane == 0) plan->active = 0;
+        const SwOut o3 = stream_walk(buf, len, P1, 0, o.nf, len, true, max_frames, desc, items, ptr, pend, nwork, res,
+                                     lane);
+        finished(o3.cnt);
         return;
     }
+    const u32 seenm = o.maxlen > seen ? o.maxlen : seen;
     u64 C = rw_pow2_clamp(mean * 1024, cmin > RW_CMIN ? cmin : RW_CMIN, cmin > cmax ? cmin : cmax);
-    u64 nch = (len - P1 + C - 1) / C;
-    // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
-    while (nch > nchunks_cap || nch * RW_D * 64 > stg_cap || nch * 64 > cand_cap) { C <<= 1; nch = (len - P1 + C - 1) / C; }
-    const u32 H = rw_window(mean, o.maxlen > seen ? o.maxlen : seen, C);
-    u64 stgn = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
-    while (stgn > 64 && nch * RW_D * stgn > stg_cap) stgn >>= 1;
-    u64 capc = H / 32;
-    while (capc > 64 && nch * capc > cand_cap) capc >>= 1;
+    // split (split_x: the first byte K2's second launch owns): part 0 = [P1, Pb >= split_x) in
+    // chunks of C >> c0_shift, at least twice the window a frame start needs (its owner walks are
+    // the latency K2's first launch waits for), part 1 = [Pb, len) in chunks of C
+    const bool split = split_x > P1 && split_x < len;
+    const u64 hneed = rw_window(mean, seenm, 4 * (u64)RW_HMAX);
+    u64 C0 = C, n0 = 0, n1 = 0, Pb = len;
+    for (;;) {
+        if (split) {
+            C0 = rw_pow2_clamp((C >> c0_shift) > 2 * hneed ? (C >> c0_shift) : 2 * hneed, RW_CMIN, C);
+            n0 = (split_x - P1 + C0 - 1) / C0;
+            Pb = P1 + n0 * C0;
+            if (Pb >= len) { Pb = len; n0 = (len - P1 + C0 - 1) / C0; }
+            n1 = Pb < len ? (len - Pb + C - 1) / C : 0;
+        } else {
+            C0 = C;
+            n0 = (len - P1 + C - 1) / C;
+        }
+        const u64 nch = n0 + n1;
+        // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
+        if (nch <= nchunks_cap && nch * RW_D * 64 <= stg_cap && nch * 64 <= cand_cap) break;
+        C <<= 1;
+    }
+    const u32 H0 = rw_window(mean, seenm, C0), H1 = rw_window(mean, seenm, C);
+    u64 stg0 = rw_pow2_clamp(2 * C0 / (mean ? mean : 1), 256, RW_CAP_STGN);
+    u64 stg1 = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
+    while ((stg0 > 64 || stg1 > 64) && (n0 * stg0 + n1 * stg1) * RW_D > stg_cap) {
+        stg0 = stg0 > 64 ? stg0 >> 1 : stg0;
+        stg1 = stg1 > 64 ? stg1 >> 1 : stg1;
+    }
+    u64 cap0 = H0 / 32, cap1 = H1 / 32;
+    while ((cap0 > 64 || cap1 > 64) && n0 * cap0 + n1 * cap1 > cand_cap) {
+        cap0 = cap0 > 64 ? cap0 >> 1 : cap0;
+        cap1 = cap1 > 64 ? cap1 >> 1 : cap1;
+    }
     if (lane == 0) {
-        plan->P = P1;
-        plan->C = C;
-        plan->H = H;
-        plan->nchunks = (u32)nch;
-        plan->capc = (u32)capc;
-        plan->stgn = (u32)stgn;
+        RwPart& a = plan->pt[0];
+        a.P = P1; a.C = C0; a.H = H0; a.n = (u32)n0; a.cbase = 0; a.capc = (u32)cap0; a.stgn = (u32)stg0;
+        a.stg_base = 0; a.cand_base = 0;
+        RwPart& b = plan->pt[1];
+        b.P = Pb; b.C = C; b.H = H1; b.n = (u32)n1; b.cbase = (u32)n0; b.capc = (u32)cap1; b.stgn = (u32)stg1;
+        b.stg_base = n0 * RW_D * stg0; b.cand_base = n0 * cap0;
+        plan->nchunks = (u32)(n0 + n1);
         plan->need_mask = (buf[P1 + 1] & 0x80u) ? 1u : 0u;                   // client frames: masked
         plan->nf = o.nf;
-        plan->nrows = 0;
+        plan->nrows[0] = plan->nrows[1] = 0;
+        plan->linked[0] = plan->linked[1] = 0;
+        plan->nw0 = 0;
+        plan->h_ent = 0;
+        plan->h_nf = 0;
+        plan->h_state = 0;
         plan->seen_max = 0;                 // this call's emit and linker fill it in
         plan->active = 1;
     }
@@ -920,22 +1009,28 @@ struct RwLink {
 __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* __restrict__ plan,
                                                          const RwRec* __restrict__ recs, const u32* __restrict__ nrec,
                                                          const unsigned long long* __restrict__ dx,
-                                                         const RwOwn* __restrict__ own, RwLink* __restrict__ lk) {
-    const u32 lane = threadIdx.x, c = blockIdx.x;
-    if (!plan->active || c >= plan->nchunks) return;
-    const u64 P = plan->P, C = plan->C;
-    const u32 H = plan->H, nchunks = plan->nchunks;
-    const u64 cs0 = P + (u64)c * C;
+                                                         const RwOwn* __restrict__ own, RwLink* __restrict__ lk,
+                                                         int part) {
+    const u32 lane = threadIdx.x, cl = blockIdx.x;                           // local chunk
+    if (!plan->active || cl >= plan->pt[part].n || (part == 1 && plan->h_state != 1)) return;
+    const RwPart& pt = plan->pt[part];
+    const u64 P = pt.P, C = pt.C;
+    const u32 H = pt.H, nchunks = plan->nchunks;
+    const u64 c = (u64)pt.cbase + cl;                                        // global chunk
+    const u64 cs0 = P + (u64)cl * C;
     const bool lastc = c + 1 == nchunks;
+    // the next chunk's size (part 0's last chunk: part 1's first)
+    const u64 Cn = (part == 0 && cl + 1 == pt.n && plan->pt[1].n) ? plan->pt[1].C : C;
     auto rl64 = [](u64 v, int i) -> u64 {
         return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, i) |
                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), i) << 32);
     };
-    // the entry: the common exit of chunk c-1's live owners
-    u64 ent = P;
+    // the entry: the common exit of chunk c-1's live owners; a part's first chunk: the part's
+    // origin (part 0) or part 0's hand-off (part 1, the chain's exact entry)
+    u64 ent = part == 0 ? P : plan->h_ent;
     bool ok = true;
-    if (c) {
-        const u64 oi = (u64)(c - 1) * RW_D + (lane & (RW_D - 1));
+    if (cl) {
+        const u64 oi = (c - 1) * RW_D + (lane & (RW_D - 1));
         const u64 d = dx[oi];
         const RwOwn o = own[oi];
         const bool live = lane < RW_D && d != 0 && !o.dead;
@@ -951,9 +1046,9 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
     RwLink L = {ent, 0, 0, 0, 0, 0};
     if (ok) {
         const u32 so = (u32)(ent - cs0);
-        const u32 n0 = nrec[4 * (u64)c], n1 = nrec[4 * (u64)c + 1];
+        const u32 n0 = nrec[4 * c], n1 = nrec[4 * c + 1];
         const u32 na = n0 < RW_S0 ? n0 : RW_S0;
-        const RwRec q = recs[(u64)c * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
+        const RwRec q = recs[c * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
         u64 m = __ballot(lane < na && q.start == so);
         u32 rcs = 0;
         u64 rexit = 0;
@@ -964,7 +1059,7 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
             rexit = rl64(q.exit, i);
             found = true;
         } else {                                                             // walks that end the stream
-            const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + (u64)c * RW_SLOTS + RW_S0;
+            const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
             const u32 nb1 = lastc ? (n1 < RW_SLAST ? n1 : RW_SLAST) : (n1 < RW_S1 ? n1 : RW_S1);
             for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
                 RwRec q1 = {};
@@ -984,7 +1079,7 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
             if (rcs >> 31) {
                 L.flags = 1 | 2 | 4;                                         // the walk ends in the window
             } else {
-                const u64 oi = (u64)c * RW_D + (lane & (RW_D - 1));
+                const u64 oi = c * RW_D + (lane & (RW_D - 1));
                 const u64 d = dx[oi];
                 const RwOwn o = own[oi];
                 const u64 mo = __ballot(lane < RW_D && d == rexit);
@@ -994,9 +1089,9 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
                     const u32 ocs = (u32)__builtin_amdgcn_readlane((int)o.cs, i);
                     const u64 oexit = rl64(o.exit, i);
                     const bool ends = (ocs >> 31) != 0 || oexit >= len;
-                    if (!dead && (ends || (oexit >= cs0 + C && oexit - cs0 < 2 * C && !lastc))) {
+                    if (!dead && (ends || (oexit >= cs0 + C && oexit - (cs0 + C) < Cn && !lastc))) {
                         L.nb = ocs & 0x7FFFFFFFu;
-                        L.oi = (u32)((u64)c * RW_D + (u64)i);
+                        L.oi = (u32)(c * RW_D + (u64)i);
                         L.flags = 1 | (ends ? 4 : 0);
                     }
                 }
@@ -1009,29 +1104,33 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
 // one block of RW_PS_T threads: the prefix sum of the chain's frame counts and the emit rows
 #define RW_PS_T 1024
 __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, RwPlan* __restrict__ plan,
-                                                             const RwLink* __restrict__ lk, u64* __restrict__ tab) {
+                                                             const RwLink* __restrict__ lk, u64* __restrict__ tab,
+                                                             const RwOwn* __restrict__ own, int part) {
     __shared__ u32 s_stop;
     __shared__ u32 s_bad;
     __shared__ u64 s_wsum[RW_PS_T / 64];
     __shared__ u64 s_carry;
     const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (!plan->active) return;
-    const u32 nchunks = plan->nchunks, stgn = plan->stgn;
-    if (tid == 0) { s_stop = nchunks; s_bad = 0; s_carry = plan->nf; }
+    if (!plan->active || (part == 1 && plan->h_state != 1)) return;
+    const RwPart& pt = plan->pt[part];
+    const u32 n = pt.n, cb = pt.cbase, stgn = pt.stgn;
+    // part 0 of a split hands the chain over to part 1 when no chunk of it ends the walk
+    const bool has_next = part == 0 && plan->pt[1].n != 0;
+    if (tid == 0) { s_stop = n; s_bad = 0; s_carry = part == 0 ? plan->nf : plan->h_nf; }
     __syncthreads();
     // the first chunk that is invalid or ends the chain
-    for (u32 c = tid; c < nchunks; c += RW_PS_T) {
-        const u32 f = lk[c].flags;
+    for (u32 c = tid; c < n; c += RW_PS_T) {
+        const u32 f = lk[cb + c].flags;
         if (!(f & 1) || (f & 4)) atomicMin(&s_stop, c);
     }
     __syncthreads();
     const u32 stop = s_stop;
-    if (stop >= nchunks || !(lk[stop].flags & 1)) return;                   // the serial linker runs
+    if (stop >= n ? !has_next : !(lk[cb + stop].flags & 1)) return;         // the serial linker runs
     // frame counts of chunks [0, stop): nfc before each, max_frames never reached on the way
     for (u32 t0 = 0; t0 <= stop; t0 += RW_PS_T) {
         const u32 c = t0 + tid;
         RwLink L = {};
-        if (c <= stop) L = lk[c];
+        if (c <= stop && c < n) L = lk[cb + c];
         const u64 cnt = c < stop ? (u64)L.cnt_w + L.nb : 0;
         u64 x = cnt;                                                         // inclusive wave scan
 #pragma unroll
@@ -1044,15 +1143,15 @@ __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, Rw
         u64 before = s_carry;
         for (u32 w = 0; w < wv; ++w) before += s_wsum[w];
         const u64 nfc = before + x - cnt;
+        const u64 cs0 = pt.P + (u64)c * pt.C;
         if (c < stop) {
             if (nfc + cnt >= max_frames) s_bad = 1;                         // max_frames mid-chain: serial
-            u64* t = tab + 8 * (u64)c;
+            u64* t = tab + 8 * ((u64)cb + c);
             const u64 n_par = L.nb < stgn ? L.nb : stgn;
             t[0] = L.ent; t[1] = L.rexit; t[2] = nfc; t[3] = L.cnt_w; t[4] = L.oi; t[5] = n_par; t[6] = 0;
-            t[7] = plan->P + (u64)c * plan->C;
-        } else if (c == stop) {
-            u64* t = tab + 8 * (u64)c;
-            const u64 cs0 = plan->P + (u64)c * plan->C;
+            t[7] = cs0;
+        } else if (c == stop && stop < n) {
+            u64* t = tab + 8 * ((u64)cb + c);
             if ((L.flags & 2) || nfc + L.cnt_w >= max_frames) {             // ends in the window: group walk
                 t[0] = L.ent; t[1] = 0; t[2] = nfc; t[3] = 0; t[4] = ~0ull; t[5] = 0; t[6] = 1; t[7] = cs0;
             } else {
@@ -1066,7 +1165,20 @@ __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, Rw
         if (tid == RW_PS_T - 1) s_carry = before + x;
         __syncthreads();
     }
-    if (tid == 0 && !s_bad) plan->nrows = stop + 1;
+    if (tid == 0 && !s_bad) {
+        if (stop < n) {                                                      // the walk ends in this part
+            plan->nrows[part] = stop + 1;
+            if (part == 0) plan->h_state = 2;                                // (nw0: the last row's emit)
+        } else {                                                             // part 0 hands over
+            plan->nrows[0] = n;
+            const u64 ent = n ? own[lk[cb + n - 1].oi].exit : pt.P;
+            plan->h_ent = ent;
+            plan->h_nf = (u32)s_carry;
+            plan->nw0 = (u32)s_carry;
+            plan->h_state = 1;
+        }
+        plan->linked[part] = 1;
+    }
 }
 
 
@@ -1082,17 +1194,24 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                                                         const RwOwn* __restrict__ own, u64* __restrict__ tab,
                                                         WebsocketFrameDesc_t* __restrict__ desc,
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
-                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res) {
+                                                        u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
+                                                        int part) {
     const u32 lane = threadIdx.x;
-    if (!plan->active || plan->nrows) return;                                // linked by ws_rw_pscan_kernel
-    const u64 P = plan->P, C = plan->C;
-    const u32 H = plan->H, nchunks = plan->nchunks, stgn = plan->stgn;
-    u64 ent = P;
-    u32 nfc = plan->nf, rows = 0;
+    if (!plan->active || plan->linked[part] || (part == 1 && plan->h_state != 1)) return;   // linked by pscan
+    const RwPart& pt = plan->pt[part];
+    const u64 P = pt.P, C = pt.C;
+    const u32 H = pt.H, nchunks = plan->nchunks, stgn = pt.stgn, np = pt.n, cb = pt.cbase;
+    // part 0 of a split stops where part 1 begins and hands the chain over
+    const bool has_next = part == 0 && plan->pt[1].n != 0;
+    const u64 Pb = plan->pt[1].P;
+    u64 ent = part == 0 ? P : plan->h_ent;
+    u32 nfc = part == 0 ? plan->nf : plan->h_nf, rows = 0;
     bool last = false;
+    u32 cnt_end = 0;                                                         // the count a finishing walk wrote
+    bool ended_walk = false;
     auto row = [&](u64 a0, u64 a1, u64 a2, u64 a3, u64 a4, u64 a5, u64 a6, u64 a7) {
         if (lane == 0) {
-            u64* t = tab + 8 * (u64)rows;
+            u64* t = tab + 8 * ((u64)cb + rows);
             t[0] = a0; t[1] = a1; t[2] = a2; t[3] = a3; t[4] = a4; t[5] = a5; t[6] = a6; t[7] = a7;
         }
         ++rows;
@@ -1102,13 +1221,13 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     // (a skipped chunk, a chunk walked here) reloads at its new chunk.
     constexpr u32 RW_LK = 8;
     u32 steps = 0, mx = 0;
-    while (!last && ent < len && steps <= nchunks + 1) {
-        const u64 c0 = (ent - P) / C;
+    while (!last && ent < len && steps <= np + 1 && !(has_next && ent >= Pb)) {
+        const u64 c0 = (ent - P) / C;                                        // local chunk
         // lane l < RW_LK: the record counts of chunk c0 + l (read back per chunk by readlane)
         u32 n0v = 0, n1v = 0;
         {
             const u64 cl = c0 + (lane < RW_LK ? lane : 0);
-            const u64 cc = cl < nchunks ? cl : (nchunks ? nchunks - 1 : 0);
+            const u64 cc = cb + (cl < np ? cl : (np ? np - 1 : 0));
             n0v = nrec[4 * cc];
             n1v = nrec[4 * cc + 1];
         }
@@ -1117,7 +1236,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
         RwOwn oo[RW_LK];
 #pragma unroll
         for (u32 k = 0; k < RW_LK; ++k) {                                   // clamped: in-range loads
-            const u64 cc = c0 + k < nchunks ? c0 + k : (nchunks ? nchunks - 1 : 0);
+            const u64 cc = cb + (c0 + k < np ? c0 + k : (np ? np - 1 : 0));
             q[k] = recs[cc * RW_SLOTS + (lane < RW_S0 ? lane : 0)];
             dd[k] = dx[cc * RW_D + (lane & (RW_D - 1))];
             oo[k] = own[cc * RW_D + (lane & (RW_D - 1))];
@@ -1125,15 +1244,16 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
         bool reload = false;
 #pragma unroll
         for (u32 k = 0; k < RW_LK; ++k) {
-            if (reload || last || ent >= len) break;
-            const u64 c = (ent - P) / C, cs0 = P + c * C;
+            if (reload || last || ent >= len || (has_next && ent >= Pb)) break;
+            const u64 c = (ent - P) / C, cs0 = P + c * C;                    // local chunk
             if (c != c0 + k) break;                                          // left the run: reload
             ++steps;
             bool found = false;
             RwRec r = {};
-            if (c < nchunks && ent - cs0 < H) {
+            const u64 gcx = (u64)cb + c;                                     // global chunk
+            if (c < np && ent - cs0 < H) {
                 const u32 so = (u32)(ent - cs0);
-                const bool lastc = c + 1 == nchunks;
+                const bool lastc = gcx + 1 == nchunks;
                 const u32 n0k = (u32)__builtin_amdgcn_readlane((int)n0v, (int)k);
                 const u32 n1k = (u32)__builtin_amdgcn_readlane((int)n1v, (int)k);
                 const u32 na = n0k < RW_S0 ? n0k : RW_S0;
@@ -1146,7 +1266,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                              ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(q[k].exit >> 32), i) << 32);
                     found = true;
                 } else {                                                     // walks that end the stream
-                    const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + c * RW_SLOTS + RW_S0;
+                    const RwRec* r1 = lastc ? recs + (u64)nchunks * RW_SLOTS : recs + gcx * RW_SLOTS + RW_S0;
                     const u32 nb1 = lastc ? (n1k < RW_SLAST ? n1k : RW_SLAST) : (n1k < RW_S1 ? n1k : RW_S1);
                     for (u32 k0 = 0; k0 < nb1 && !found; k0 += 64) {
                         RwRec q1 = {};
@@ -1183,7 +1303,7 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                         last = (ocs >> 31) != 0 || oexit >= len || (u64)nfc + cnt_w + nb >= max_frames;
                         u64 n_par = nb < stgn ? nb : stgn;
                         if (last && (u64)nfc + cnt_w + n_par > max_frames) n_par = max_frames - nfc - cnt_w;
-                        row(ent, r.exit, nfc, cnt_w, c * RW_D + (u64)i, n_par, last ? 1ull : 0ull, cs0);
+                        row(ent, r.exit, nfc, cnt_w, gcx * RW_D + (u64)i, n_par, last ? 1ull : 0ull, cs0);
                         nfc += cnt_w + nb;
                         ent = oexit;
                         continue;
@@ -1194,20 +1314,37 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
             const SwOut o = stream_walk(buf, len, ent, 0, nfc, cs0 + C < len ? cs0 + C : len, false, max_frames, desc,
                                         items, ptr, pend, nwork, res, lane, plan->sample_out, true);
             if (o.maxlen > mx) mx = o.maxlen;
-            if (o.ended) { last = true; break; }                            // (the walk finished the stream)
-            if (o.next <= ent) { steps = nchunks + 2; break; }               // (cannot happen: no progress)
+            if (o.ended) { last = true; ended_walk = true; cnt_end = o.cnt; break; }   // (it finished the stream)
+            if (o.next <= ent) { steps = np + 2; break; }                    // (cannot happen: no progress)
             ent = o.next;
             nfc = o.nf;
             reload = true;                                                   // its frames may cross chunks
         }
     }
-    if (!last) {                                                             // safety: walk whatever is left
+    const bool handoff = !last && has_next && ent >= Pb && ent < len;
+    if (!last && !handoff) {                                                 // safety: walk whatever is left
         const SwOut o = stream_walk(buf, len, ent, 0, nfc, len, true, max_frames, desc, items, ptr, pend, nwork, res,
                                     lane, nullptr, true);
         if (o.maxlen > mx) mx = o.maxlen;
+        ended_walk = true;
+        cnt_end = o.cnt;
     }
     rw_note_max(plan, mx, lane);
-    if (lane == 0) plan->nrows = rows;
+    if (lane == 0) {
+        plan->nrows[part] = rows;
+        if (part == 0) {
+            if (handoff) {
+                plan->h_ent = ent;
+                plan->h_nf = nfc;
+                plan->nw0 = nfc;
+                plan->h_state = 1;
+            } else {
+                plan->h_state = 2;
+                if (ended_walk) plan->nw0 = cnt_end;                         // (else: the last row's emit writes it)
+            }
+        }
+        plan->linked[part] = 1;
+    }
 }
 
 WsOpt ws_stream_rw{1};          // "stream_rw": chunk-parallel walk for long streams, linked on the device
@@ -1216,6 +1353,12 @@ WsOpt ws_stream_rw_cmax{22};    // "stream_rw_cmax": log2 of the largest chunk (
                                 // against 8.19-8.21 at 8 MiB and 8.14-8.15 at 2 MiB, profiles/r04_stream_cmax_ab.log)
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
+WsOpt ws_stream_split{16};      // "stream_split": device-planned walks: K2's first launch takes this many 256ths of
+                                // the pieces, the walk past them runs beside it on a side stream (0: no split)
+WsOpt ws_stream_split_wait{0};  // "stream_split_wait": part 1's walk starts after the plan (0), part 0's owner
+                                // walks (1) or part 0's emit (2)
+WsOpt ws_stream_side_prio{0};   // "stream_side_prio": the split walk's side stream priority: 0 default, 1 least, 2 greatest
+WsOpt ws_stream_c0{2};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
@@ -1324,14 +1467,14 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
     const u32 need_mask = (hb[1] & 0x80u) ? 1u : 0u;
     const u64 threads = nchunks * (H / RW_TPOS);
     hipLaunchKernelGGL(ws_rw_cand_kernel, dim3((u32)((threads + 255) / 256)), dim3(256), 0, st, d_buf, len, P, C, H,
-                       (u32)nchunks, need_mask, cand, nrec, capc, (const RwPlan*)nullptr);
+                       (u32)nchunks, need_mask, cand, nrec, capc, (const RwPlan*)nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_cand_kernel launch", e);
     const u32 r2_blocks = (u32)std::min<u64>((nchunks * capc + 255) / 256, 4096);  // grid-stride
     hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(r2_blocks), dim3(256), 0, st, d_buf, len, P, C, H, (u32)nchunks,
-                       need_mask, cand, capc, recs, nrec, dx, (const RwPlan*)nullptr);
+                       need_mask, cand, capc, recs, nrec, dx, (const RwPlan*)nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_spec_kernel launch", e);
     hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((nchunks * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len, P,
-                       C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr);
+                       C, (u32)nchunks, need_mask, dx, own, stg, stgn, (const RwPlan*)nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_own_kernel launch", e);
     if ((e = hipMemcpyAsync(hw + 256, w + 256, b_host, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
@@ -1400,7 +1543,7 @@ static int rw_walk(WsSlot& slot, unsigned char* d_buf, u64 len, u64 P, u32 nf, u
         if ((e = hipMemcpyAsync(tab, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, st)) != hipSuccess)
             return ws_set_err("hipMemcpyAsync(stream chain)", e);
         hipLaunchKernelGGL(ws_rw_emit_kernel, dim3(nblk), dim3(64), 0, st, d_buf, len, max_frames, tab, own, stg, stgn,
-                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, (const RwPlan*)nullptr);
+                           d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res, (RwPlan*)nullptr, 0);
         if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("ws_rw_emit_kernel launch", e);
     }
     // `ht` is pageable host memory read by the copy above: complete it before returning
@@ -1437,10 +1580,23 @@ static RwDevLayout rw_dev_layout(u64 len) {
     return L;
 }
 
+// The split of a device-planned walk (round 6): K2 runs as two launches, over
+// the pieces before and after piece p0, and the walk of the stream past them (part 1) runs on a
+// side stream while the first launch streams. Side-stream work joins the caller's stream through
+// events (eager and captured calls alike: in a capture the events are the graph's fork and join).
+struct RwSplit {
+    u64 p0 = 0;                  // K2's first launch: pieces [0, p0); 0 = no split
+    u64 x = 0;                   // the first stream byte the second launch owns (piece p0's start)
+    hipStream_t side = nullptr;
+    hipEvent_t ev[3] = {};       // part-1 start, part 0 linked + emitted, part 1 emitted
+    int wait = 0;                // part 1's R1-R3 start after: 0 the plan, 1 part 0's R3, 2 part 0's emit
+    u32 c0_shift = 2;            // part 0's chunks: C >> c0_shift (at least twice the window)
+};
+
 static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, WebsocketFrameDesc_t* d_desc,
                           const PieceWs& Pw, WebsocketSegResult_t* d_res, hipStream_t st, SdState* sd,
                           unsigned char* w, const RwDevLayout& L, int fresh = 0, u64* d_seg = nullptr,
-                          SdMirror* mirror = nullptr) {
+                          SdMirror* mirror = nullptr, const RwSplit* sp = nullptr) {
     RwPlan* plan = reinterpret_cast<RwPlan*>(w + L.o_plan);
     u32* nrec = reinterpret_cast<u32*>(w + L.o_nrec);
     unsigned long long* dx = reinterpret_cast<unsigned long long*>(w + L.o_dx);
@@ -1449,34 +1605,91 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     u64* tab = reinterpret_cast<u64*>(w + L.o_tab);
     u32* stg = reinterpret_cast<u32*>(w + L.o_stg);
     u64* cand = reinterpret_cast<u64*>(w + L.o_cand);
+    RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
     const int cmax_log = ws_stream_rw_cmax;                                  // one read per call
     const u64 cmax = cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX;
+    const bool split = sp && sp->p0;
     hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
-                       fresh, d_seg, Pw.disorder, mirror);
-    // R1 grid-stride, R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
-    hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(RW_R1_GRID), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
-                       cand, nrec, 0u, (const RwPlan*)plan);
-    hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(RW_R2_GRID), dim3(256), 0, st, d_buf, len, (u64)0, (u64)1, (u32)64, 0u, 0u,
-                       (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan);
-    hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0, st, d_buf, len,
-                       (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u, (const RwPlan*)plan);
-    if (ws_stream_plink) {          // the chunk-parallel linker; the serial one below exits if it linked
-        RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
-        hipLaunchKernelGGL(ws_rw_plink_kernel, dim3((u32)L.nch_cap), dim3(64), 0, st, len, (const RwPlan*)plan,
-                           (const RwRec*)recs, (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, lk);
-        hipLaunchKernelGGL(ws_rw_pscan_kernel, dim3(1), dim3(RW_PS_T), 0, st, max_frames, plan, (const RwLink*)lk, tab);
+                       fresh, d_seg, Pw.disorder, mirror, split ? sp->x : 0ull, split ? sp->c0_shift : 0u);
+    // one part's candidate, window and owner walks; its linking and emit
+    auto rwalk = [&](hipStream_t s, int part) {
+        // R1 and R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
+        hipLaunchKernelGGL(ws_rw_cand_kernel, dim3(RW_R1_GRID), dim3(256), 0, s, d_buf, len, (u64)0, (u64)1, (u32)64, 0u,
+                           0u, cand, nrec, 0u, (const RwPlan*)plan, part);
+        hipLaunchKernelGGL(ws_rw_spec_kernel, dim3(RW_R2_GRID), dim3(256), 0, s, d_buf, len, (u64)0, (u64)1, (u32)64, 0u,
+                           0u, (const u64*)cand, 0u, recs, nrec, dx, (const RwPlan*)plan, part);
+        hipLaunchKernelGGL(ws_rw_own_kernel, dim3((u32)((L.nch_cap * RW_D + RW_OWN_T - 1) / RW_OWN_T)), dim3(RW_OWN_T), 0,
+                           s, d_buf, len, (u64)0, (u64)1, 0u, 0u, (const unsigned long long*)dx, own, stg, 0u,
+                           (const RwPlan*)plan, part);
+    };
+    auto rlink = [&](hipStream_t s, int part) {
+        if (ws_stream_plink) {      // the chunk-parallel linker; the serial one below exits if it linked
+            hipLaunchKernelGGL(ws_rw_plink_kernel, dim3((u32)L.nch_cap), dim3(64), 0, s, len, (const RwPlan*)plan,
+                               (const RwRec*)recs, (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own,
+                               lk, part);
+            hipLaunchKernelGGL(ws_rw_pscan_kernel, dim3(1), dim3(RW_PS_T), 0, s, max_frames, plan, (const RwLink*)lk, tab,
+                               (const RwOwn*)own, part);
+        }
+        hipLaunchKernelGGL(ws_rw_link_kernel, dim3(1), dim3(64), 0, s, d_buf, len, max_frames, plan, (const RwRec*)recs,
+                           (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, tab, d_desc, Pw.items,
+                           Pw.ptr, Pw.npieces, Pw.nwork, d_res, part);
+        hipLaunchKernelGGL(ws_rw_emit_kernel, dim3((u32)(L.nch_cap + 2)), dim3(64), 0, s, d_buf, len, max_frames,
+                           (const u64*)tab, (const RwOwn*)own, (const u32*)stg, 0u, d_desc, Pw.items, Pw.ptr,
+                           Pw.npieces, Pw.nwork, d_res, plan, part);
+    };
+    if (!split) {
+        rwalk(st, 0);
+        rlink(st, 0);
+        if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("stream walk (device) launch", e);
+        return 0;
     }
-    hipLaunchKernelGGL(ws_rw_link_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, plan, (const RwRec*)recs,
-                       (const u32*)nrec, (const unsigned long long*)dx, (const RwOwn*)own, tab, d_desc, Pw.items,
-                       Pw.ptr, Pw.npieces, Pw.nwork, d_res);
-    hipLaunchKernelGGL(ws_rw_emit_kernel, dim3((u32)(L.nch_cap + 2)), dim3(64), 0, st, d_buf, len, max_frames,
-                       (const u64*)tab, (const RwOwn*)own, (const u32*)stg, 0u, d_desc, Pw.items, Pw.ptr, Pw.npieces,
-                       Pw.nwork, d_res, (const RwPlan*)plan);
+#define RW_TRY(call, what) do { if ((e = (call)) != hipSuccess) return ws_set_err(what, e); } while (0)
+    if (sp->wait == 0) {
+        RW_TRY(hipEventRecord(sp->ev[0], st), "hipEventRecord(stream split)");
+        RW_TRY(hipStreamWaitEvent(sp->side, sp->ev[0], 0), "hipStreamWaitEvent(stream split)");
+        rwalk(sp->side, 1);
+    }
+    rwalk(st, 0);
+    if (sp->wait == 1) {
+        RW_TRY(hipEventRecord(sp->ev[0], st), "hipEventRecord(stream split)");
+        RW_TRY(hipStreamWaitEvent(sp->side, sp->ev[0], 0), "hipStreamWaitEvent(stream split)");
+        rwalk(sp->side, 1);
+    }
+    rlink(st, 0);
+    RW_TRY(hipEventRecord(sp->ev[1], st), "hipEventRecord(stream split)");
+    RW_TRY(hipStreamWaitEvent(sp->side, sp->ev[1], 0), "hipStreamWaitEvent(stream split)");
+    if (sp->wait >= 2) rwalk(sp->side, 1);
+    rlink(sp->side, 1);
+    RW_TRY(hipEventRecord(sp->ev[2], sp->side), "hipEventRecord(stream split)");
+#undef RW_TRY
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("stream walk (device) launch", e);
     return 0;
+}
+
+// K2 after a device-planned walk: one launch, or (split) the pieces before p0 with the count
+// part 0 left in the plan, then — once part 1 is emitted — the pieces from p0 on
+std::atomic<unsigned long long> ws_stat_stream_splits{0};   // raw-stream calls whose K2 ran split (since load)
+static int rw_unmask(const WsLaunch& L, const PieceWs& Pw, u32 gen, const RwSplit* sp, const RwPlan* plan) {
+    if (!sp || !sp->p0) return ws_launch_piece_unmask(L, Pw, gen);
+    ++ws_stat_stream_splits;
+    const u64 cpp = 1ull << (PIECE_SHIFT_S - 4);                             // 16-B chunks per piece
+    PieceWs A = Pw;
+    A.npieces = sp->p0;
+    A.c_hi = std::min<u64>(Pw.c_hi, sp->p0 * cpp);
+    A.nwork = const_cast<u32*>(&plan->nw0);
+    int rc = ws_launch_piece_unmask(L, A, gen);
+    if (rc) return rc;
+    hipError_t e = hipStreamWaitEvent(L.stream, sp->ev[2], 0);
+    if (e != hipSuccess) return ws_set_err("hipStreamWaitEvent(stream split join)", e);
+    PieceWs B = Pw;
+    B.ptr = Pw.ptr + sp->p0;
+    B.pbase = Pw.pbase + sp->p0;
+    B.npieces = Pw.npieces - sp->p0;
+    B.c_lo = std::max<u64>(Pw.c_lo, sp->p0 * cpp);
+    return ws_launch_piece_unmask(L, B, gen);
 }
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,
@@ -1564,15 +1777,30 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         return e2 == hipSuccess ? 0 : ws_set_err("ws_stream_pass_kernel launch", e2);
     };
     const int nr0 = ws_stream_rounds, nr = nr0 >= 1 && nr0 <= 64 ? nr0 : 4;
+    // the split of a device-planned walk (RwSplit): K2's first launch owns pieces [0, p0)
+    RwSplit SP;
+    unsigned char* const rw_w = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
+    const RwPlan* const rw_plan = reinterpret_cast<const RwPlan*>(rw_w + RL.o_plan);
+    if (dev_layout) {
+        const int spl = ws_stream_split, sw = ws_stream_split_wait, c0 = ws_stream_c0;   // one read each
+        const int pr = ws_stream_side_prio;
+        if (spl > 0 && spl < 256 && Pw.npieces >= 2) {
+            SP.p0 = std::max<u64>(1, Pw.npieces * (u64)spl / 256);
+            const u64 lead0 = reinterpret_cast<uintptr_t>(d_buf) & 15;
+            SP.x = (SP.p0 << PIECE_SHIFT_S) - lead0;
+            SP.wait = sw >= 0 && sw <= 2 ? sw : 0;
+            SP.c0_shift = c0 >= 0 && c0 <= 6 ? (u32)c0 : 2u;
+            if ((rc = slot.side(&SP.side, SP.ev, pr >= 0 && pr <= 2 ? pr : 0))) return rc;
+        }
+    }
     if (dev_rw) {
         // a replay whose previous replay's chunk walk saw lengths that keep changing skips the
         // rounds on the device (they exit at once) and the plan kernel starts the walk at 0
         if ((rc = rounds(nr, false, 0, 1))) return rc;
-        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
-                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 2, d_seg)))
+        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd, rw_w, RL, 2, d_seg, nullptr, &SP)))
             return rc;
         *A.state_ok = true;
-        return ws_launch_piece_unmask(L, Pw, gen);
+        return rw_unmask(L, Pw, gen, &SP, rw_plan);
     }
     if (!host_rw) {
         if ((rc = rounds(nr, true, 0, 0))) return rc;
@@ -1600,10 +1828,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     if (rw_opt == 1 && __atomic_load_n(&hm->walk_hint, __ATOMIC_RELAXED) == 1) {
         ++ws_stat_stream_skips;
         *A.state_ok = true;
-        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,
-                                 reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 1, d_seg, dm)))
+        if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd, rw_w, RL, 1, d_seg, dm, &SP)))
             return rc;
-        return ws_launch_piece_unmask(L, Pw, gen);
+        return rw_unmask(L, Pw, gen, &SP, rw_plan);
     }
     u32 tag = ws_next_gen();
     if ((rc = rounds(1, false, tag, 0)) || (rc = published(tag))) return rc;
@@ -1616,9 +1843,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
         const u64 P = hm->P;
         const u32 nf = hm->nf;
         if (len - P >= RW_MIN && rw_opt == 1) {                              // lengths keep changing:
-            if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd,    // the device walks
-                                     reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD, RL, 0, d_seg, dm)))
+            if ((rc = rw_walk_device(d_buf, len, max_frames, d_desc, Pw, d_res, st, sd, rw_w, RL, 0, d_seg, dm,
+                                     &SP)))                                  // the device walks
                 return rc;
+            return rw_unmask(L, Pw, gen, &SP, rw_plan);
         } else if (len - P >= RW_MIN) {                                      // ... the host follows
             if ((rc = rw_walk(slot, d_buf, len, P, nf, max_frames, d_desc, Pw, d_res, st))) return rc;
         } else {
