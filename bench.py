@@ -123,6 +123,8 @@ class Workload:
         "cfg5": (1 << 22, 0, 1024, 2, 5, 16),    # 256K messages x 16 fragments
         # not a BASELINE config: cfg5 with 1000-B fragments (bodies off the 16-B grid)
         "cfg5u": (1 << 22, 0, 1000, 2, 6, 16),
+        # cfg3's length mix as ONE global batch sharded over the ranks (strong scaling, STRONG)
+        "cfg3s": (1 << 20, 1, 0, 0, 3, 16),
     }
     DESCRIPTION = {
         "cfg1": "16 masked text frames x 125 B",
@@ -131,6 +133,7 @@ class Workload:
         "cfg4": "1M masked binary frames x 64 KiB per GPU (8M over 8 GPUs)",
         "cfg5": "256K messages x 16 continuation frames x 1 KiB (16-frame segments = messages)",
         "cfg5u": "256K messages x 16 continuation frames x 1000 B (bodies off the 16-B grid)",
+        "cfg3s": "cfg3's length mix as one global batch, byte-balanced shards",
     }
 
     @classmethod
@@ -591,10 +594,34 @@ def end_to_end(wl, runs=2):
     pageable = {"value": round(wl.payload_bytes / dtp / 2**30, 2), "unit": "GiB/s", "ms": round(dtp * 1e3, 2),
                 "runs": 2, "host_buffer": "pageable (numpy)", "verified": bool(np.array_equal(hp, hb.numpy()))}
     del hp
+    # the multi-device entry on the same pinned arena (websocketframeBatchDecodeHostMulti): every
+    # visible GPU takes a byte-balanced range over its own PCIe link; on a one-GPU box the device
+    # listed twice (its two ranges one after the other: the cost of the split itself)
+    ndev = torch.cuda.device_count()
+    devs = np.arange(ndev, dtype=np.int32) if ndev > 1 else np.zeros(2, dtype=np.int32)
+    hm = torch.empty(wl.wire_bytes, dtype=torch.uint8, pin_memory=True)
+    hm.copy_(hb)
+
+    def once_multi():
+        rc = lib.websocketframeBatchDecodeHostMulti(hm.data_ptr(), wl.wire_bytes, so.ctypes.data, sl.ctypes.data,
+                                                    wl.nseg, wl.fps, desc.data_ptr(), res.data_ptr(),
+                                                    devs.ctypes.data, len(devs))
+        if rc:
+            raise RuntimeError(lib.websocketframeGpuLastError().decode())
+    once_multi()                                       # warm: every device's slots
+    t0 = time.perf_counter()
+    once_multi()
+    dtm = (time.perf_counter() - t0)
+    multi = {"value": round(wl.payload_bytes / dtm / 2**30, 2), "unit": "GiB/s", "ms": round(dtm * 1e3, 2),
+             "runs": 1, "devices": devs.tolist(), "host_buffer": "pinned",
+             "path": "websocketframeBatchDecodeHostMulti: byte-balanced segment ranges, one per device, each "
+                     "websocketframeBatchDecodeHost's pipeline from its own host thread",
+             "verified": bool(torch.equal(hm, hb))}
+    del hm
     return {"value": round(wl.payload_bytes / dt / 2**30, 2), "unit": "GiB/s", "ms": round(dt * 1e3, 2),
             "runs": runs, "host_buffer": "pinned (hipHostMalloc via torch pin_memory)",
             "path": "websocketframeBatchDecodeHost: H2D | decode | D2H over 64 MiB groups, 3 streams",
-            "pageable": pageable}, runs + 1
+            "pageable": pageable, "multi_device": multi}, runs + 1
 
 
 def granted_cpus():
@@ -725,32 +752,51 @@ def cpu_baseline(sample, threads=None, min_seconds=2.0, op="decode", frames_per_
     return out
 
 
-STRONG = {"cfg4": 8 << 20}     # config -> global frames of its strong-scaling batch (BASELINE configs[3])
+STRONG = {"cfg4": 8 << 20,      # config -> global frames of its strong-scaling batch (BASELINE configs[3])
+          "cfg3s": 8 << 20}     # cfg3's length mix as one global batch (mixed lengths: byte-balanced shards)
+STRONG_ROUND_BYTES = 64 << 30   # default HBM budget per round for mixed-length batches (wire bytes)
+
+
+def strong_layout(config, n_total):
+    """The global batch of a strong-scaling config on the host: every frame's payload and wire
+    length (generator frames 0 .. n_total - 1, util_amd/synth.py) and every rx segment's wire
+    bytes — what util_amd/dist.py:run_shard balances the shards and bounds the rounds by"""
+    from util_amd import synth
+    n, pk, fl, bk, seed, fps = Workload.CONFIGS[config]
+    assert n_total % fps == 0, "strong mode: whole segments"
+    plen = synth.plens(pk, fl, seed, n_total, 0)
+    wl = synth.wirelens(plen)
+    seg_bytes = wl.reshape(-1, fps).sum(axis=1, dtype=np.uint64).astype(np.int64)
+    return plen, wl, seg_bytes
 
 
 def run_strong(args, dev, world, rank):
     """BASELINE configs[3] as strong scaling: ONE global batch (8 M x 64 KiB masked frames,
-    16-frame rx segments, 549.9 GB of wire) split over the ranks by segment ranges
-    (util_amd/dist.py:run_shard); each rank generates its share where it decodes it (frames by
-    global index, websocketframeSynthDeviceRange), in rounds of at most --round-frames frames
-    (1 M = 68.7 GB of wire by default: 8 rounds on one GPU, one on each of 8). Per round:
-    generate, `warmup` decodes, `steps` decodes timed with HIP events at the region's two ends,
-    one more if needed so the buffer holds plaintext, the output hash, the generator check.
-    A step = one pass over the whole batch: ms_per_step = max over ranks of the sum over its
-    rounds of the per-call decode time; value = the batch's payload / that."""
+    16-frame rx segments, 549.9 GB of wire; or --config cfg3s: 8 M frames of cfg3's length mix)
+    split over the ranks by segment ranges balanced by wire bytes (util_amd/dist.py:run_shard,
+    SURVEY §8e); each rank generates its share where it decodes it (frames by global index,
+    websocketframeSynthDeviceRange), in rounds of at most --round-frames frames and (mixed
+    lengths) --round-bytes wire bytes (defaults: 1 M frames = 68.7 GB of cfg4: 8 rounds on one GPU,
+    one on each of 8). Per round: generate, `warmup` decodes, `steps` decodes timed with HIP events
+    at the region's two ends, one more if needed so the buffer holds plaintext, the output hash,
+    the generator check. A step = one pass over the whole batch: ms_per_step = max over ranks of
+    the sum over its rounds of the per-call decode time; value = the batch's payload / that."""
     import torch
     from util_amd import dist as D
-    from util_amd import synth
     from util_amd import wsframe as W
     n_total = args.global_frames or STRONG[args.config]
     n, pk, fl, bk, seed, fps = Workload.CONFIGS[args.config]
-    assert pk == 0, "strong mode: fixed-size frames"
     nseg_total = n_total // fps
+    plen_all, wl_all, seg_bytes = strong_layout(args.config, n_total)
+    foff_all = np.zeros(n_total + 1, dtype=np.int64)
+    np.cumsum(wl_all.astype(np.int64), out=foff_all[1:])
     per_round = max(1, (args.round_frames or (1 << 20)) // fps)
-    first_seg, count = D.segment_shard(nseg_total, world, rank)
-    max_segs = min(per_round, count) if count else 1
-    wirelen = int(synth.wirelens(np.array([fl], np.uint64))[0])
-    cap = max_segs * fps * wirelen
+    max_bytes = args.round_bytes or (STRONG_ROUND_BYTES if pk else None)
+    cuts = D.shard_cuts(nseg_total, world, seg_bytes)
+    first_seg, count = cuts[rank], cuts[rank + 1] - cuts[rank]
+    rounds = D.shard_rounds(first_seg, count, per_round, seg_bytes, max_bytes)
+    max_segs = max([1] + [nr for _, nr in rounds])
+    cap = max([0] + [int(foff_all[(s + nr) * fps] - foff_all[s * fps]) for s, nr in rounds])
     buf = torch.empty(cap + 256, dtype=torch.uint8, device=dev)
     buf[cap:].zero_()
     desc = torch.empty(max_segs * fps * 32, dtype=torch.uint8, device=dev)
@@ -762,11 +808,15 @@ def run_strong(args, dev, world, rank):
 
     def decode_round(s, nseg):
         nf = nseg * fps
-        foff = torch.arange(nf, dtype=torch.int64, device=dev) * wirelen
+        f0 = s * fps
+        foff_h = foff_all[f0:f0 + nf + 1] - foff_all[f0]
+        nbytes = int(foff_h[-1])
+        foff = torch.from_numpy(np.ascontiguousarray(foff_h[:-1])).to(dev)
         so = foff[::fps].contiguous()
-        sl = torch.full((nseg,), fps * wirelen, dtype=torch.int64, device=dev)
-        b = buf[:nf * wirelen + 256]
-        W.synth_device(b, foff, nf, pk, fl, bk, seed, first_frame=s * fps)
+        sl = torch.from_numpy(np.ascontiguousarray(seg_bytes[s:s + nseg])).to(dev)
+        b = buf[:nbytes + 256]
+        b[nbytes:].zero_()
+        W.synth_device(b, foff, nf, pk, fl, bk, seed, first_frame=f0)
 
         def call():
             W.batch_decode_device(b, so, sl, fps, desc, res)
@@ -784,37 +834,50 @@ def run_strong(args, dev, world, rank):
         hsh.zero_()
         mm.zero_()
         W.frame_hash_device(b, desc, res, nseg, fps, hsh)
-        W.synth_verify_device(b, foff, nf, pk, fl, seed, True, mm, first_frame=s * fps)
+        W.synth_verify_device(b, foff, nf, pk, fl, seed, True, mm, first_frame=f0)
         r = res[:nseg * 16].view(torch.int64).view(-1, 2)
         frames = int((r[:, 1] & 0xFFFFFFFF).sum())
-        bad_status = int(((r[:, 1] >> 32) != 0).sum()) + int(int(r[:, 0].sum()) != nf * wirelen)
+        bad_status = int(((r[:, 1] >> 32) != 0).sum()) + int(int(r[:, 0].sum()) != nbytes)
         torch.cuda.synchronize()
-        return dict(frames=frames, payload=nf * fl, wire=nf * wirelen, errors=int(mm.item()) + bad_status,
-                    hash=int(hsh.item()) & 0xFFFFFFFFFFFFFFFF, seconds=ms / 1e3)
+        return dict(frames=frames, payload=int(plen_all[f0:f0 + nf].sum()), wire=nbytes,
+                    errors=int(mm.item()) + bad_status, hash=int(hsh.item()) & 0xFFFFFFFFFFFFFFFF, seconds=ms / 1e3)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     t0 = time.perf_counter()
-    loc, glob = D.run_shard(nseg_total, world, rank, per_round, decode_round, device=dev)
+    loc, glob = D.run_shard(nseg_total, world, rank, per_round, decode_round, device=dev, seg_bytes=seg_bytes,
+                            max_bytes_per_round=max_bytes)
     wall = D.allreduce([time.perf_counter() - t0], op="max", device=dev)[0]
     step_s = glob["seconds"]
     algo = glob["wire"] + glob["payload"]
+    rw = glob["rank_wire"]
+    desc_txt = ("8M masked binary frames x 64 KiB" if args.config == "cfg4" else
+                "%d frames, payload uniform from {125 B, 1500 B, 64 KiB}" % n_total if pk else
+                "%d frames x %d B" % (n_total, fl))
     out = {
-        "metric": "WebSocket unmask GiB/s (device-resident), 8M x 64KiB frames sharded across GPUs",
+        "metric": "WebSocket unmask GiB/s (device-resident), 8M x 64KiB frames sharded across GPUs"
+        if args.config == "cfg4" else "WebSocket unmask GiB/s (device-resident), one mixed-length batch sharded "
+                                      "across GPUs",
         "value": round(glob["payload"] / step_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded counter-based generator util_amd/csrc/ws_synth.h, each shard generated in HBM "
                 "by global frame index)",
-        "config": {"workload": "8M masked binary frames x 64 KiB, 16-frame rx segments, one batch sharded by segment "
-                               "ranges", "config": args.config, "global_frames": n_total,
+        "config": {"workload": desc_txt + ", 16-frame rx segments, one batch sharded by byte-balanced segment "
+                                          "ranges", "config": args.config, "global_frames": n_total,
                    "global_wire_bytes": glob["wire"], "global_payload_bytes": glob["payload"],
-                   "rounds_per_rank": loc["rounds"], "frames_per_round": per_round * fps, "alloc": args.alloc,
-                   "parallelism": "segment-range shards over %d GPU(s), no data-path collective" % world},
+                   "rounds_per_rank": loc["rounds"], "frames_per_round": per_round * fps,
+                   "round_bytes_max": max_bytes, "alloc": args.alloc,
+                   "rank_wire_bytes": rw,
+                   "rank_wire_imbalance": round(max(rw) / (sum(rw) / world), 6) if sum(rw) else None,
+                   "parallelism": "byte-balanced segment-range shards over %d GPU(s), no data-path collective"
+                                  % world},
         "roofline": {"bound": "hbm", "achieved": round(algo / world / step_s / 1e9, 1), "peak": PEAK_HBM_GBS,
                      "unit": "GB/s per GPU", "frac": round(algo / world / step_s / 1e9 / PEAK_HBM_GBS, 4),
                      "traffic": None, "kernel": "ws_piece_unmask_kernel", "algo_bytes_per_step": algo,
-                     "algo_bytes_per_launch": per_round * fps * (wirelen + fl),
+                     "algo_bytes_per_launch": int(foff_all[(rounds[0][0] + rounds[0][1]) * fps] -
+                                                  foff_all[rounds[0][0] * fps]) +
+                     int(plen_all[rounds[0][0] * fps:(rounds[0][0] + rounds[0][1]) * fps].sum()) if rounds else 0,
                      "kernel_ms_mean": round(step_s * 1e3 / max(1, loc["rounds"]), 4),
                      "timed": "per round: HIP events at the two ends of `steps` back-to-back decode calls; step = "
                               "sum over the rank's rounds, max over ranks (generation, hashing and checks between "
@@ -825,9 +888,7 @@ def run_strong(args, dev, world, rank):
         "wall_s_incl_generation": round(wall, 2),
         "cpu_baseline": None,
     }
-    if rank == 0:
-        emit(out)
-    return 0 if out["verified"] else 1
+    return out, 0 if out["verified"] else 1
 
 
 def run_inflight(args, wl0, dev, world, rank):
@@ -1156,6 +1217,8 @@ def main():
                     help="strong-scaling configs (cfg4): frames of the global batch (default 8M)")
     ap.add_argument("--round-frames", type=int, default=None,
                     help="strong-scaling configs: frames per round on one GPU (default 1M = 68.7 GB of wire)")
+    ap.add_argument("--round-bytes", type=int, default=None,
+                    help="strong-scaling configs: wire bytes per round at most (default: 64 GiB for mixed lengths)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="decode: also time K independent batches of the config in flight together, one HIP "
                          "stream each (a reactor with successive rx batches), reported as the 'inflight' field "
@@ -1261,7 +1324,7 @@ def main():
         e2e, flips = end_to_end(wl)
         wl.decodes += flips
         e2e_mism = wl.verify(expect_plain=(wl.decodes % 2 == 1))
-        e2e["verified"] = e2e_mism == 0
+        e2e["verified"] = e2e_mism == 0 and e2e["pageable"]["verified"] and e2e["multi_device"]["verified"]
         mism += e2e_mism
     if args.inflight > 1:
         inflight, m = run_inflight(args, wl, dev, world, rank)

@@ -183,6 +183,21 @@ WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHost(unsigned char* h_buf, unsig
                                                      unsigned int max_frames, WebsocketFrameDesc_t* h_desc,
                                                      WebsocketSegResult_t* h_res, int device);
 
+/* The same on several devices (one host rx arena, every device's PCIe link carrying a share;
+ * net_reactor.c:484-500 keeps every connection's m_inbuf in host memory): ascending,
+ * non-overlapping segments are cut into ndev contiguous ranges of about equal bytes (at the
+ * segment boundary nearest to each equal share) and each range runs
+ * websocketframeBatchDecodeHost's pipeline on devices[i] from its own host thread; results land
+ * in h_desc / h_res exactly where the one-device call puts them. A device may be listed more than
+ * once (its ranges then run one after the other). Any other segment layout (unordered,
+ * overlapping) or ndev == 1 is the one-device call on devices[0]. Synchronous; returns 0 or the
+ * first failing range's error (websocketframeGpuLastError names its device). */
+WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHostMulti(unsigned char* h_buf, unsigned long long buflen,
+                                                          const unsigned long long* h_seg_off,
+                                                          const unsigned long long* h_seg_len, unsigned int nseg,
+                                                          unsigned int max_frames, WebsocketFrameDesc_t* h_desc,
+                                                          WebsocketSegResult_t* h_res, const int* devices, int ndev);
+
 /* One raw rx stream of any size (a single connection's inbuf; no frame offsets from the
  * host): identical results to websocketframeBatchDecodeDevice with the one segment
  * [0, len) (descriptors d_desc[0..], result d_res[0]); WEBSOCKET_BATCH_PAD readable bytes

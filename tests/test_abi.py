@@ -39,7 +39,7 @@ def test_exports_exactly_the_declared_symbols():
     kernel stubs, no bench or calibration entry points, no C++ symbols)"""
     lib = util_amd.load_lib()
     declared = header_symbols()
-    assert len(declared) == 19
+    assert len(declared) == 20
     assert sorted(_lib.EXPORTS) == declared
     assert dynamic_symbols(_lib.LIB_PATH) == set(declared)
     for s in declared:

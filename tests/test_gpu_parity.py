@@ -259,6 +259,34 @@ def test_host_path_pipelined(dev, chunk_mb):
         W.set_option("host_chunk_mb", 64)
 
 
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], [0] * 7])
+def test_host_path_multi_device(dev, devices):
+    """websocketframeBatchDecodeHostMulti on one box: the ascending segments cut into byte-balanced
+    ranges, one per listed device (here the one GPU, repeated: its ranges run one after the other
+    through the same pipeline), odd segment counts and mixed segment sizes so the cuts fall
+    between unequal neighbours; bit-exact vs the oracle, slots past n_frames zeroed; unordered
+    segments fall back to the one-device call"""
+    rng = np.random.default_rng(13 + len(devices))
+    wire, so, sl = random_stream(rng, 2001, max_frame=30000)
+    W.set_option("host_chunk_mb", 1)
+    try:
+        for tag, (s_, l_) in (("ordered", (so, sl)), ("unordered", None)):
+            if s_ is None:
+                perm = rng.permutation(len(so))
+                s_, l_ = [so[i] for i in perm], [sl[i] for i in perm]
+            hb = wire.copy()
+            gd, gr = W.batch_decode_host_multi(hb, s_, l_, 16, devices)
+            ob = wire.copy()
+            od, orr = oracle_segments(ob, s_, l_, 16)
+            assert np.array_equal(gr, orr), tag
+            assert np.array_equal(used_descs(gd, gr, 16), used_descs(od, orr, 16)), tag
+            assert np.array_equal(hb, ob), tag
+            for k in range(len(s_)):
+                assert not gd[k * 16 + int(gr[k]["n_frames"]):(k + 1) * 16].view(np.uint8).any(), tag
+    finally:
+        W.set_option("host_chunk_mb", 64)
+
+
 def test_host_path_unordered_segments(dev):
     """segments out of buffer order: decoded as one group spanning all of them"""
     rng = np.random.default_rng(12)

@@ -36,7 +36,7 @@ REFERENCE_EXPORTS = [
 # every symbol include/wsframe_amd.h + include/wsframe_amd_channel.h declare: the whole
 # dynamic symbol table of libwsframe_amd.so
 EXPORTS = REFERENCE_EXPORTS + [
-    "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost",
+    "websocketframeBatchDecodeDevice", "websocketframeBatchDecodeHost", "websocketframeBatchDecodeHostMulti",
     "websocketframeBatchEncodeDevice", "websocketframeBatchReassembleDevice",
     "websocketframeBatchReassembleDeviceEx", "websocketframeStreamDecodeDevice",
     "websocketframeGpuLastError", "websocketframeGpuSetOption", "websocketframeGpuGetStat",
@@ -105,6 +105,8 @@ def load_lib():
     lib.websocketframeBatchEncodeDevice.argtypes = [vp, vp, u32, vp, u64, vp, vp]
     lib.websocketframeBatchDecodeHost.restype = i32
     lib.websocketframeBatchDecodeHost.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, i32]
+    lib.websocketframeBatchDecodeHostMulti.restype = i32
+    lib.websocketframeBatchDecodeHostMulti.argtypes = [vp, u64, vp, vp, u32, u32, vp, vp, vp, i32]
     lib.websocketframeGpuLastError.restype = C.c_char_p
     lib.websocketframeGpuLastError.argtypes = []
     lib.websocketframeGpuSetOption.restype = i32

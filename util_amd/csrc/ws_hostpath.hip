@@ -14,7 +14,10 @@
 // thread's current HIP device is restored before returning.
 #include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
+
+#include <string>
 
 #include "ws_common.h"
 
@@ -182,4 +185,71 @@ drain:
         if (e2 != hipSuccess && !rc) rc = ws_set_err("hipStreamSynchronize", e2);
     }
     return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Several devices on one host rx arena (net_reactor.c:484-500): the
+// ascending segments are cut into `ndev` contiguous ranges of about equal bytes (the segment
+// boundary nearest to each equal share), and each range runs websocketframeBatchDecodeHost's
+// pipeline on its own device from its own host thread, so every device's PCIe link carries its
+// share (one pinned arena served by up to ndev links). A device listed twice runs its ranges one
+// after the other (its pipeline is locked per device). Any other segment layout is decoded on
+// devices[0] alone. Returns the first range's error (every range is drained first).
+extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchDecodeHostMulti(unsigned char* h_buf, unsigned long long buflen,
+                                                                     const u64* h_seg_off, const u64* h_seg_len,
+                                                                     unsigned int nseg, unsigned int max_frames,
+                                                                     WebsocketFrameDesc_t* h_desc,
+                                                                     WebsocketSegResult_t* h_res, const int* devices,
+                                                                     int ndev) {
+    if (nseg == 0) return 0;
+    if (!devices || ndev <= 0 || !h_seg_off || !h_seg_len)
+        return ws_set_msg("websocketframeBatchDecodeHostMulti: invalid argument");
+    bool ordered = true;
+    u64 prev_end = 0, total = 0;
+    for (u32 s = 0; s < nseg; ++s) {
+        if (h_seg_off[s] < prev_end) ordered = false;
+        prev_end = h_seg_off[s] + h_seg_len[s];
+        total += h_seg_len[s];
+    }
+    if (!ordered || ndev == 1 || nseg < 2)
+        return websocketframeBatchDecodeHost(h_buf, buflen, h_seg_off, h_seg_len, nseg, max_frames, h_desc, h_res,
+                                             devices[0]);
+    // cuts: the segment boundary nearest to each equal share of the bytes
+    const u32 nd = (u32)std::min<u64>((u64)ndev, nseg);
+    std::vector<u32> cut(nd + 1, 0);
+    cut[nd] = nseg;
+    {
+        u64 acc = 0;
+        u32 s = 0;
+        for (u32 r = 1; r < nd; ++r) {
+            const long double t = (long double)total * r / nd;
+            while (s < nseg && (long double)(acc + h_seg_len[s]) <= t) acc += h_seg_len[s++];
+            // acc <= t < acc + len[s]: the nearer boundary
+            if (s < nseg && (long double)(acc + h_seg_len[s]) - t < t - (long double)acc) acc += h_seg_len[s++];
+            cut[r] = std::max(s, cut[r - 1]);
+        }
+    }
+    std::vector<int> rc(nd, 0);
+    std::vector<std::string> err(nd);
+    auto part = [&](u32 r) {
+        const u32 a = cut[r], b = cut[r + 1];
+        if (a < b) {
+            rc[r] = websocketframeBatchDecodeHost(h_buf, buflen, h_seg_off + a, h_seg_len + a, b - a, max_frames,
+                                                  h_desc + (size_t)a * max_frames, h_res + a, devices[r]);
+            if (rc[r]) err[r] = websocketframeGpuLastError();            // (the error text is per thread)
+        }
+    };
+    std::vector<std::thread> th;
+    th.reserve(nd);
+    for (u32 r = 1; r < nd; ++r) th.emplace_back(part, r);
+    part(0);
+    for (auto& t : th) t.join();
+    for (u32 r = 0; r < nd; ++r)
+        if (rc[r]) {
+            char msg[320];
+            snprintf(msg, sizeof(msg), "websocketframeBatchDecodeHostMulti (device %d): %s", devices[r], err[r].c_str());
+            ws_set_msg(msg);
+            return rc[r];
+        }
+    return 0;
 }

@@ -32,7 +32,13 @@ def byte_balanced_cuts(seg_len, world):
     total = csum[-1]
     cuts = [0]
     for r in range(1, world):
-        cuts.append(int(np.searchsorted(csum, total * r / world, side="left")))
+        # the segment boundary nearest to the r-th equal share: every rank's bytes then lie within
+        # one segment of total / world
+        t = total * r / world
+        i = int(np.searchsorted(csum, t, side="left"))
+        if 0 < i <= n and t - csum[i - 1] < csum[i] - t:
+            i -= 1
+        cuts.append(min(i, n))
     cuts.append(n)
     for i in range(1, len(cuts)):      # monotone
         cuts[i] = max(cuts[i], cuts[i - 1])
@@ -93,18 +99,30 @@ def scatter_from_root(send, recv, nbytes, root=0):
     return dt
 
 
-def segment_shard(nseg_total, world, rank):
-    """contiguous, balanced segment range [first, first+count) of `rank` (equal-size
-    segments: balanced by bytes too)"""
-    return frame_shard(nseg_total, world, rank)
+def shard_cuts(nseg_total, world, seg_bytes=None):
+    """world+1 segment cut indices of one global batch: byte-balanced when the segments' wire
+    bytes are given (balance by bytes, not frame count — a mixed-length batch), else
+    equal segment counts"""
+    if seg_bytes is None:
+        return [frame_shard(nseg_total, world, r)[0] for r in range(world)] + [nseg_total]
+    assert len(seg_bytes) == nseg_total
+    return byte_balanced_cuts(seg_bytes, world)
 
 
-def shard_rounds(first, count, max_per_round):
+def shard_rounds(first, count, max_per_round, seg_bytes=None, max_bytes=None):
     """[(first_segment, nseg), ...] covering [first, first + count) in rounds of at most
-    max_per_round segments (the shard's HBM budget)"""
+    max_per_round segments and, when the segments' bytes are given, at most max_bytes wire
+    bytes (the shard's HBM budget; a segment larger than that is a round of its own)"""
     out, s = [], first
+    csum = None
+    if seg_bytes is not None and max_bytes:
+        csum = np.concatenate([[0], np.cumsum(np.asarray(seg_bytes[first:first + count], dtype=np.int64))])
     while s < first + count:
         n = min(max_per_round, first + count - s)
+        if csum is not None:
+            base = csum[s - first]
+            fit = int(np.searchsorted(csum, base + max_bytes, side="right")) - 1 - (s - first)
+            n = max(1, min(n, fit))
         out.append((s, n))
         s += n
     return out
@@ -153,16 +171,20 @@ def allreduce_u64(values, device=None):
     return [sum(int(t[4 * k + i]) << (16 * i) for i in range(4)) & 0xFFFFFFFFFFFFFFFF for k in range(len(vals))]
 
 
-def run_shard(nseg_total, world, rank, max_seg_per_round, decode_round, device=None):
+def run_shard(nseg_total, world, rank, max_seg_per_round, decode_round, device=None, seg_bytes=None,
+              max_bytes_per_round=None):
     """Decode this rank's share of one global batch of nseg_total segments, round by round.
     decode_round(first_segment, nseg) -> dict(frames, payload, wire, errors, hash, seconds)
     decodes segments [first, first + nseg) (global indices; it generates them where it
     decodes them) and returns its counts, its output hash and its timed decode seconds.
-    Returns (local totals, global totals: sums over ranks, seconds = max over ranks)."""
-    first, count = segment_shard(nseg_total, world, rank)
+    seg_bytes (optional, every segment's wire bytes): the shards are byte-balanced and the rounds
+    hold at most max_bytes_per_round bytes. Returns (local totals, global totals: sums over
+    ranks, seconds = max over ranks; global["rank_wire"]: every rank's wire bytes)."""
+    cuts = shard_cuts(nseg_total, world, seg_bytes)
+    first, count = cuts[rank], cuts[rank + 1] - cuts[rank]
     loc = dict(frames=0, payload=0, wire=0, errors=0, hash=0, seconds=0.0, rounds=0, segments=count,
                first_segment=first)
-    for s, n in shard_rounds(first, count, max_seg_per_round):
+    for s, n in shard_rounds(first, count, max_seg_per_round, seg_bytes, max_bytes_per_round):
         r = decode_round(s, n)
         for k in ("frames", "payload", "wire", "errors"):
             loc[k] += int(r[k])
@@ -172,5 +194,8 @@ def run_shard(nseg_total, world, rank, max_seg_per_round, decode_round, device=N
     frames, payload, wire, errors, h = allreduce_u64([loc["frames"], loc["payload"], loc["wire"], loc["errors"],
                                                       loc["hash"]], device=device)
     secs = allreduce([loc["seconds"]], op="max", device=device)[0]
-    glob = dict(frames=frames, payload=payload, wire=wire, errors=errors, hash=h, seconds=secs)
+    onehot = [0] * world
+    onehot[rank] = loc["wire"]
+    rank_wire = allreduce_u64(onehot, device=device)
+    glob = dict(frames=frames, payload=payload, wire=wire, errors=errors, hash=h, seconds=secs, rank_wire=rank_wire)
     return loc, glob

@@ -207,6 +207,23 @@ def batch_decode_host(buf, seg_off, seg_len, max_frames, device=0):
     return desc, res[:nseg]
 
 
+def batch_decode_host_multi(buf, seg_off, seg_len, max_frames, devices):
+    """websocketframeBatchDecodeHostMulti: buf (numpy uint8, modified in place) decoded on several
+    devices (a byte-balanced range each; a device may repeat). Returns (desc, res) as
+    batch_decode_host does."""
+    nseg = len(seg_off)
+    seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    seg_len = np.ascontiguousarray(seg_len, dtype=np.uint64)
+    desc = np.zeros(max(1, nseg * max_frames), dtype=DESC_DTYPE)
+    res = np.zeros(max(1, nseg), dtype=SEGRES_DTYPE)
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    rc = load_lib().websocketframeBatchDecodeHostMulti(buf.ctypes.data, buf.nbytes, seg_off.ctypes.data,
+                                                       seg_len.ctypes.data, nseg, max_frames, desc.ctypes.data,
+                                                       res.ctypes.data, devs.ctypes.data, len(devs))
+    check(rc, "websocketframeBatchDecodeHostMulti")
+    return desc, res[:nseg]
+
+
 def synth_device(buf, frame_off, nframes, plen_kind, fixed_len, b0_kind, seed, stream=None, first_frame=0):
     """websocketframeSynthDeviceRange (libwsframe_amd_bench.so): bench/test input generated in
     HBM — generator frames first_frame .. first_frame + nframes - 1 at buf + frame_off[i]"""
