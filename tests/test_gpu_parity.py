@@ -270,10 +270,8 @@ def test_host_path_multi_device(dev, devices):
     wire, so, sl = random_stream(rng, 2001, max_frame=30000)
     W.set_option("host_chunk_mb", 1)
     try:
-        for tag, (s_, l_) in (("ordered", (so, sl)), ("unordered", None)):
-            if s_ is None:
-                perm = rng.permutation(len(so))
-                s_, l_ = [so[i] for i in perm], [sl[i] for i in perm]
+        perm = rng.permutation(len(so))
+        for tag, s_, l_ in (("ordered", so, sl), ("unordered", [so[i] for i in perm], [sl[i] for i in perm])):
             hb = wire.copy()
             gd, gr = W.batch_decode_host_multi(hb, s_, l_, 16, devices)
             ob = wire.copy()

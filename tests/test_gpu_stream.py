@@ -446,7 +446,7 @@ def test_two_raw_streams_in_parallel_threads(dev):
 def split_opts():
     """restores the split options after a test that changes them"""
     yield
-    W.set_option("stream_split", 16)
+    W.set_option("stream_split", 24)
     W.set_option("stream_split_wait", 0)
     W.set_option("stream_c0", 2)
     W.set_option("stream_rw", 1)
@@ -502,8 +502,9 @@ def test_stream_split_long_frames_and_host_path(dev, split_opts):
 
 
 def test_stream_split_captured(dev, split_opts):
-    """a captured raw-stream decode with the split (the side stream forks and joins inside the
-    graph): replays of changing bytes, a max_frames stop in part 0, bit-exact each time"""
+    """a captured raw-stream decode with the split option set: captured calls do not split (a
+    graph's branches run one after the other), replays of changing bytes and a max_frames stop
+    where part 0 would end are bit-exact each time"""
     W.set_option("stream_split", 32)
     rng = np.random.default_rng(621)
     wire = long_stream(rng, 32 << 20, mix3)

@@ -1353,11 +1353,11 @@ WsOpt ws_stream_rw_cmax{22};    // "stream_rw_cmax": log2 of the largest chunk (
                                 // against 8.19-8.21 at 8 MiB and 8.14-8.15 at 2 MiB, profiles/r04_stream_cmax_ab.log)
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
-WsOpt ws_stream_split{16};      // "stream_split": device-planned walks: K2's first launch takes this many 256ths of
-                                // the pieces, the walk past them runs beside it on a side stream (0: no split)
+WsOpt ws_stream_split{24};      // "stream_split": eager device-planned walks: K2's first launch takes this many 256ths
+                                // of the pieces, the walk past them runs beside it on a side stream (0: no split)
 WsOpt ws_stream_split_wait{0};  // "stream_split_wait": part 1's walk starts after the plan (0), part 0's owner
                                 // walks (1) or part 0's emit (2)
-WsOpt ws_stream_side_prio{0};   // "stream_side_prio": the split walk's side stream priority: 0 default, 1 least, 2 greatest
+WsOpt ws_stream_side_prio{1};   // "stream_side_prio": the split walk's side stream priority: 0 default, 1 least, 2 greatest
 WsOpt ws_stream_c0{2};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
@@ -1607,8 +1607,11 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     u64* cand = reinterpret_cast<u64*>(w + L.o_cand);
     RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
     const int cmax_log = ws_stream_rw_cmax;                                  // one read per call
-    const u64 cmax = cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX;
     const bool split = sp && sp->p0;
+    // a split walk's part 1 runs beside K2: chunks twice the usual largest (fewer windows for R1 to
+    // scan beside the stream; its longer owner walks are hidden), part 0 = that >> c0_shift
+    const u64 cmax = std::min<u64>((cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX) << (split ? 1 : 0),
+                                   RW_CMAX);
     hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
@@ -1781,7 +1784,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     RwSplit SP;
     unsigned char* const rw_w = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
     const RwPlan* const rw_plan = reinterpret_cast<const RwPlan*>(rw_w + RL.o_plan);
-    if (dev_layout) {
+    // (eager calls only: a captured graph's branches are not run concurrently — the split measured
+    // 8.57-8.59 ms against 8.06-8.08 unsplit for cfg3 replays, profiles/r06_stream_split_ab.log)
+    if (dev_layout && !capture) {
         const int spl = ws_stream_split, sw = ws_stream_split_wait, c0 = ws_stream_c0;   // one read each
         const int pr = ws_stream_side_prio;
         if (spl > 0 && spl < 256 && Pw.npieces >= 2) {
