@@ -258,7 +258,9 @@ WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long va
  * calls since load that skipped the pass rounds because the previous chunk walk on the stream saw
  * lengths that keep changing), "stream_splits" (raw-stream calls since load whose unmask
  * ran as two launches beside the split walk, option "stream_split"), "capture_adoptions" (graph captures since load that took over the
- * workspace slot of a destroyed graph whose replays had all finished); with the option
+ * workspace slot of a destroyed graph whose replays had all finished), "capture_adoption_refusals" (captures
+ * since load that passed over such a slot because a replay of its graph was still queued), "k2_windows" (the
+ * piece windows of the most recent unmask launch: 1 << the "piece_win" rule's choice); with the option
  * "k2_timing" set, "k2_ns" / "k2_calls" (the summed duration and count of the piece
  * path's unmask launches since the option was set, from HIP events around each launch;
  * reading them waits for those launches). Returns 0, or -1 for an unknown name. */

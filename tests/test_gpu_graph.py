@@ -383,10 +383,11 @@ def test_capture_does_not_adopt_a_slot_whose_replay_is_queued(dev):
     # (the runtime may wait for the pending launch when the graph is destroyed: then the replay
     # has finished here and adopting its slot is right)
     pending = not torch.cuda.current_stream().query()
-    a0 = W.get_stat("capture_adoptions")
+    a0, f0 = W.get_stat("capture_adoptions"), W.get_stat("capture_adoption_refusals")
     g2 = capture(side)                           # the replay is still queued behind the spin
-    if pending:
+    if pending:                                  # the guard ran: it refused the dead slot
         assert W.get_stat("capture_adoptions") == a0
+        assert W.get_stat("capture_adoption_refusals") > f0
     torch.cuda.synchronize()
     assert np.array_equal(d[:n].cpu().numpy(), ob)
     d[:n].copy_(src)
@@ -400,11 +401,14 @@ def test_capture_does_not_adopt_a_slot_whose_replay_is_queued(dev):
     a1 = W.get_stat("capture_adoptions")
     g3 = capture(side)                           # every replay done: a dead slot is adopted
     assert W.get_stat("capture_adoptions") == a1 + 1
-    print("replay pending at the second capture:", pending)
     d[:n].copy_(src)
     g3.replay()
     torch.cuda.synchronize()
     assert np.array_equal(d[:n].cpu().numpy(), ob)
+    if not pending:
+        #  everything above ran, but the refusal itself was not reached: this runtime
+        # waited for the queued replay when the graph was destroyed — reported, not passed silently
+        pytest.skip("the runtime finished the queued replay at graph destruction: replays_done() was not exercised")
 
 
 @pytest.mark.parametrize("path", [1, 2], ids=["fused", "three_kernel"])

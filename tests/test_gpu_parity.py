@@ -375,6 +375,29 @@ def test_window_mappings(dev, decode_path, opt, val):
         W.set_option("piece_lds", 0)
 
 
+def test_window_rule_automatic_four_windows(dev):
+    """the automatic rule (piece_win -1) on a >= 16 GiB batch of one frame length: the
+    first call on a stream has no advice and takes two windows, the next one (advised: frames of
+    one length) four (stat k2_windows); 4 M x 4 KiB frames (17.2 GB): after the first call every
+    payload is the generator's plaintext, after the second the wire is back, descriptors equal
+    websocketframeDecode's for every frame both times"""
+    import bench
+    st = torch.cuda.Stream(dev)                       # a fresh stream: a workspace slot without advice
+    with torch.cuda.stream(st):
+        wl = bench.Workload.make("cfg2", dev, nframes=4 << 20)
+        torch.cuda.synchronize()
+        assert wl.wire_bytes >= 16 << 30
+        wins = []
+        for k in range(2):
+            wl.decode(stream=st)
+            st.synchronize()
+            wins.append(W.get_stat("k2_windows"))
+            assert wl.verify(expect_plain=(k == 0)) == 0, k
+            wl.check_descs()
+    assert wins == [2, 4], wins
+    wl.free()
+
+
 def test_cfg4_shape_vs_oracle(dev, decode_path):
     """cfg4's layout (64 KiB masked frames, 16-frame rx segments, 64-bit length form) at reduced
     size, bit-exact vs the oracle: generator frames taken from the middle of the global batch

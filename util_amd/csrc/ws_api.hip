@@ -38,6 +38,7 @@ size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips,
     ws_stat_stream_splits;
 extern std::atomic<unsigned long long> ws_stat_adoptions;
+extern std::atomic<unsigned long long> ws_stat_k2_windows;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
@@ -149,6 +150,8 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuGetStat(const char* name, uns
     else if (!strcmp(name, "stream_splits")) *value = ws_stat_stream_splits.load();
     else if (!strcmp(name, "workspace_bytes")) *value = ws_workspace_bytes_total();
     else if (!strcmp(name, "capture_adoptions")) *value = ws_stat_adoptions.load();
+    else if (!strcmp(name, "k2_windows")) *value = ws_stat_k2_windows.load();
+    else if (!strcmp(name, "capture_adoption_refusals")) *value = ws_stat_adoption_refusals.load();
 
     else return -1;
     return 0;
@@ -267,6 +270,7 @@ static void slot_free(WsStreamWs& w) {
 }
 
 std::atomic<unsigned long long> ws_stat_adoptions{0};
+std::atomic<unsigned long long> ws_stat_adoption_refusals{0};   // dead slots not adopted: a replay still queued
 static void capture_slot_destroyed(void* p) { reinterpret_cast<WsStreamWs*>(p)->dead.store(1); }
 
 // a destroyed graph's slot may be adopted only once every replay that was launched has finished:
@@ -341,7 +345,10 @@ static int stream_slot(WsDevState* ds, hipStream_t stream, WsStreamWs** out) {
             continue;
         }
         if (w.captured && w.dead.load() && !w.busy) {
-            if (!adopt && cap && replays_done(w)) adopt = &w;
+            if (!adopt && cap) {
+                if (replays_done(w)) adopt = &w;
+                else ++ws_stat_adoption_refusals;
+            }
             continue;
         }
         if (!w.captured) {
@@ -445,7 +452,13 @@ WsSlot::~WsSlot() { release(); }
 
 void WsSlot::release() {
     if (!w) return;
-    // a captured call ends with an event record node (replays_done)
+    // a captured call ends with an event record node (replays_done). Assumption: once
+    // hipGraphLaunch has queued a replay, w->done reads as not ready until that replay's record
+    // node has run — HIP's host-side launch resets the event's status at enqueue. If the record
+    // only changed the status when the node ran, a query between launch and node would report the
+    // previous replay's completed record and the slot could be adopted too early; the capture test
+    // (tests/test_gpu_graph.py, refusal stat) checks the refusal whenever the runtime leaves a
+    // destroyed graph's replay queued.
     if (w->captured && w->done && capturing(st)) (void)hipEventRecord(w->done, st);
     std::lock_guard<std::mutex> lk(g_dev_mu);
     --w->busy;

@@ -697,6 +697,7 @@ static u32 piece_wshift(u64 npieces, u32 g0) {
 
 // K2 over the pieces of a scanned batch; advice (device view of pinned host memory, may be
 // null): K2 turns K1's non-uniform count into the host's stride hint for the next call
+std::atomic<unsigned long long> ws_stat_k2_windows{0};   // windows of the most recent K2 launch (stat "k2_windows")
 int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* advice, u32 g0) {
     if (!P.npieces) return 0;
     size_t tslot = 0;
@@ -704,6 +705,7 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
     const u32 wshift = piece_wshift(P.npieces, g0);
+    ws_stat_k2_windows = 1ull << wshift;
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;
     if (P.segr)

@@ -880,7 +880,10 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
                                                         SdMirror* __restrict__ mirror, u64 split_x, u32 c0_shift) {
     const u32 lane = threadIdx.x;
-    const u32 seen = plan->seen_max;        // the previous walk's longest frame (0 before the first: WS_AUX_ZERO)
+    // the previous device walk's longest frame: 0 before the first (the plan lies in the WS_AUX_ZERO range,
+    // zeroed when the aux buffer is allocated or a capture adopts the slot; the host-linked walk's
+    // scratch starts after it, rw_scratch)
+    const u32 seen = plan->seen_max;
     // fresh 2 (captured calls): the previous replay's hint decides, as the passes saw it
     const int dev = fresh == 2;
     if (dev) fresh = sd->walk_hint != 0;
@@ -1371,12 +1374,14 @@ struct RwScratch {
     void* h = nullptr;
 };
 
-// (the aux head holds the pass loop's state: the walk's scratch starts after it)
+// (the aux head holds the pass loop's state and the 256 B after it the device walk's plan,
+// RwPlan: the host-linked walk's device scratch starts after both, so a slot that serves both
+// kinds of call never hands the plan this walk's leftovers — ADVICE r05)
 static int rw_scratch(WsSlot& slot, size_t dbytes, size_t hbytes, RwScratch* out) {
     WsAux A;
-    const int rc = slot.aux(WS_AUX_HEAD + dbytes, WS_AUX_HEAD + hbytes, &A);
+    const int rc = slot.aux(WS_AUX_ZERO + dbytes, WS_AUX_HEAD + hbytes, &A);
     if (rc) return rc;
-    out->d = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
+    out->d = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_ZERO;
     out->h = reinterpret_cast<unsigned char*>(A.h) + WS_AUX_HEAD;
     return 0;
 }

@@ -1,7 +1,8 @@
 // ws_walker.hip — variant "walker": one wavefront walks one rx segment and
 // unmasks each frame as it goes (net_reactor.c:515-526 loop, fused).
 //
-// Kept as an A/B variant of the split design (ws_split.hip): every frame is a
+// Kept as option path=1 and as the unmask kernel's fallback for batches with no pieces (the
+// default is the piece path, ws_piece.hip: K1 walks, K2 unmasks 16 KiB pieces): every frame is a
 // dependent round (header -> payload loads -> stores) inside one long-lived wave,
 // and on CDNA vmcnt retires loads and stores in issue order, so each frame's loads
 // also wait for the previous frame's stores. Measured ~5.2 TB/s on cfg2 vs ~6 TB/s
