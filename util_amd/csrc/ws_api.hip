@@ -39,6 +39,7 @@ extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks
     ws_stat_stream_splits;
 extern std::atomic<unsigned long long> ws_stat_adoptions;
 extern std::atomic<unsigned long long> ws_stat_k2_windows;
+extern std::atomic<unsigned long long> ws_stat_adoption_refusals;
 
 int ws_set_err(const char* what, hipError_t e) {
     snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
