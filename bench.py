@@ -330,12 +330,24 @@ def run_encode(args, dev, world, rank):
         "cpu_baseline": cpu_encode_baseline(wl, args.cpu_threads or granted_cpus()[0])
         if rank == 0 and world == 1 and not args.no_cpu else None,
     }
+    if getattr(args, "cpu_defer", False):      # run_paths: timed on the CPU after every GPU path
+        out["_cpu_later"] = (lambda smp=encode_cpu_sample(wl): cpu_encode_baseline(
+            None, args.cpu_threads or granted_cpus()[0], sample=smp))
     return out, mism
 
 
-def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0):
+def encode_cpu_sample(wl, nframes=65536):
+    """the first `nframes` frames of an encode workload, copied to host memory"""
+    n = min(nframes, wl.nframes)
+    fr = wl.frames[:n * wl.W.ENC_DTYPE.itemsize].cpu().numpy().view(wl.W.ENC_DTYPE).copy()
+    src = wl.src[:n * wl.plen].cpu().numpy().copy()
+    return fr, src
+
+
+def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0, sample=None):
     """the reference's header encoder + client masking loop (oracle/ref_loop.c:ref_encode_frames)
-    on host cores, over the first `nframes` frames of the workload"""
+    on host cores, over the first `nframes` frames of the workload (or a sample taken earlier by
+    encode_cpu_sample)"""
     ref = os.path.join(REPO, "oracle", "_ref", "libwsref_loop.so")
     if not os.path.exists(ref):
         return None
@@ -343,9 +355,8 @@ def cpu_encode_baseline(wl, threads, nframes=65536, min_seconds=1.0):
     fn = lib.ref_encode_frames
     fn.restype = C.c_ulonglong
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint, C.c_void_p]
-    n = min(nframes, wl.nframes)
-    fr = wl.frames[:n * wl.W.ENC_DTYPE.itemsize].cpu().numpy().view(wl.W.ENC_DTYPE)
-    src = wl.src[:n * wl.plen].cpu().numpy()
+    fr, src = sample if sample is not None else encode_cpu_sample(wl, nframes)
+    n = len(fr)
     so = np.ascontiguousarray(fr["src_off"])
     ln = np.ascontiguousarray(fr["len"])
     key = np.ascontiguousarray(fr["mask_key"])
@@ -522,6 +533,10 @@ def run_reasm(args, dev, world, rank):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(wl.host_sample(262144), args.cpu_threads or None, op="reasm", frames_per_segment=wl.fps)
+    later = None
+    if getattr(args, "cpu_defer", False):      # run_paths: timed on the CPU after every GPU path
+        later = (lambda smp=wl.host_sample(262144), fps=wl.fps: cpu_baseline(smp, args.cpu_threads or None,
+                                                                             op="reasm", frames_per_segment=fps))
     out_json = {
         "metric": metric,
         "value": round(wl.payload_bytes * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
@@ -547,6 +562,8 @@ def run_reasm(args, dev, world, rank):
         "output_hash": "%016x" % ghash,
         "cpu_baseline": cpu,
     }
+    if later is not None:
+        out_json["_cpu_later"] = later
     return out_json, mism
 
 
@@ -1088,12 +1105,18 @@ def run_paths(args, dev):
     import copy
     import torch
     from util_amd import wsframe as W
-    entries, mism = {}, 0
+    entries, mism, later = {}, 0, {}
     fns = {"decode": run_decode, "reasm": run_reasm, "stream": run_stream, "encode": run_encode}
+    only = [x for x in (args.paths or "").split(",") if x]
     for name, (op, cfg) in PATHS.items():
+        if only and name not in only:
+            continue
         a = copy.copy(args)
         a.config, a.op, a.graph, a.frames, a.fps, a.plen, a.inflight = cfg, op, False, None, None, None, 1
         a.readcache = PATH_READCACHE if op == "reasm" else 0
+        # CPU baselines run after every path is timed: the GPU never idles for seconds between
+        # paths (a decode after idle time runs its first calls slower, DESIGN §4 "Short timed regions")
+        a.cpu_defer, a.no_cpu = not args.no_cpu, True
         t0 = time.perf_counter()
         if op == "decode":
             out, m = run_decode(a, dev, 1, 0, path=DEFAULT_PATH)
@@ -1112,17 +1135,20 @@ def run_paths(args, dev):
                           "kernel_frac": rf.get("kernel_frac"), "traffic": rf.get("traffic"),
                           "timed": rf["timed"]},
              "profile": profile_check(out), "wall_s": round(time.perf_counter() - t0, 2)}
-        if out.get("cpu_baseline"):
-            e["cpu_baseline"] = out["cpu_baseline"]
+        if out.get("_cpu_later"):
+            later[name] = out.pop("_cpu_later")
         if op == "reasm":
             e["readcache_max_size"] = a.readcache
         entries[name] = e
-    if entries["decode_cfg3"]["output_hash"] != entries["stream_cfg3"]["output_hash"]:
-        mism += 1
-        entries["stream_cfg3"]["verified"] = False
-    entries["stream_cfg3"]["hash_equals_decode_cfg3"] = \
-        entries["decode_cfg3"]["output_hash"] == entries["stream_cfg3"]["output_hash"]
+    if "decode_cfg3" in entries and "stream_cfg3" in entries:
+        if entries["decode_cfg3"]["output_hash"] != entries["stream_cfg3"]["output_hash"]:
+            mism += 1
+            entries["stream_cfg3"]["verified"] = False
+        entries["stream_cfg3"]["hash_equals_decode_cfg3"] = \
+            entries["decode_cfg3"]["output_hash"] == entries["stream_cfg3"]["output_hash"]
     W.set_option("k2_timing", 0)
+    for name, fn in later.items():
+        entries[name]["cpu_baseline"] = fn()
     return entries, mism
 
 
@@ -1202,6 +1228,8 @@ def main():
     ap.add_argument("--no-paths", action="store_true",
                     help="skip the other single-GPU paths (cfg3 decode, cfg5 reassembly, cfg3 raw stream, cfg2 "
                          "encode) the default cfg2 run at N = 1 times beside the headline (`paths`)")
+    ap.add_argument("--paths", default="",
+                    help="comma list of the `paths` entries to time (default: all of %s)" % ",".join(PATHS))
     ap.add_argument("--readcache", type=int, default=0,
                     help="--op reasm: readcache_max_size (net_channel_ex.c:45-53; 0 = no limit)")
     ap.add_argument("--no-xor-stream", action="store_true", help="skip the plain XOR-stream reference run")
@@ -1332,8 +1360,6 @@ def main():
         out["inflight"] = inflight
     out["xor_stream"] = xor_stream
     out["e2e"] = e2e
-    if sample is not None:
-        out["cpu_baseline"] = cpu_baseline(sample, args.cpu_threads or None)
     if args.scatter and world > 1:                                 # SURVEY §8e (1), outside the timed region
         recv = None if rank == 0 else torch.empty(wl.wire_bytes, dtype=torch.uint8, device=dev)
         dt = D.allreduce([D.scatter_from_root(wl.buf, recv, wl.wire_bytes)], op="max", device=dev)[0]
@@ -1350,6 +1376,8 @@ def main():
         del wl
         out["paths"], m = run_paths(args, dev)
         mism += m
+    if sample is not None:                                         # host cores, after every GPU timing
+        out["cpu_baseline"] = cpu_baseline(sample, args.cpu_threads or None)
     mism = int(D.allreduce([mism], device=dev)[0])
     out["verified"] = out["verified"] and mism == 0
     out["config"]["alloc"] = args.alloc

@@ -232,8 +232,8 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * caps its blocks per CU; 0 = the CU's LDS / 7 when the previous call on the stream advised
  * frames of one length <= 16 KiB, / 6 for longer ones, and without advice / 7 for batches with
  * at least one segment per 8 pieces of 16 KiB, else / 6), "piece_win" (0..6: log2 of the windows the
- * unmask kernel streams side by side; -1 default: 2 for batches of >= 16 GiB that the previous call on
- * the stream advised as frames of one length, else 1), "seg_win" (0/1: two windows for the
+ * unmask kernel streams side by side; -1 default: 2 for batches of >= 32 GiB, and of >= 16 GiB that the
+ * previous call on the stream advised as frames of one length, else 1), "seg_win" (0/1: two windows for the
  * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
  * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",

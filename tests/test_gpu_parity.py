@@ -375,15 +375,22 @@ def test_window_mappings(dev, decode_path, opt, val):
         W.set_option("piece_lds", 0)
 
 
-def test_window_rule_automatic_four_windows(dev):
-    """the automatic rule (piece_win -1) on a >= 16 GiB batch of one frame length: the
-    first call on a stream has no advice and takes two windows, the next one (advised: frames of
-    one length) four (stat k2_windows); 4 M x 4 KiB frames (17.2 GB): after the first call every
-    payload is the generator's plaintext, after the second the wire is back, descriptors equal
-    websocketframeDecode's for every frame both times"""
+def test_window_rule_automatic_four_windows(dev, decode_path):
+    """the automatic rule (piece_win -1) on a >= 16 GiB batch of one frame length: a
+    call on a stream whose previous call advised mixed lengths takes two windows, the next one
+    (advised: frames of one length) four (stat k2_windows); 4 M x 4 KiB frames (17.2 GB): after the
+    first call every payload is the generator's plaintext, after the second the wire is back,
+    descriptors equal websocketframeDecode's for every frame both times"""
     import bench
-    st = torch.cuda.Stream(dev)                       # a fresh stream: a workspace slot without advice
+    if decode_path != -1:
+        pytest.skip("the rule is the auto path's (run once)")
+    st = torch.cuda.Stream(dev)
     with torch.cuda.stream(st):
+        # a mixed-length batch first: the stream's advice is then "not one length" (as for a first call)
+        mixed = bench.Workload.make("cfg3", dev, nframes=4096)
+        mixed.decode(stream=st)
+        st.synchronize()
+        mixed.free()
         wl = bench.Workload.make("cfg2", dev, nframes=4 << 20)
         torch.cuda.synchronize()
         assert wl.wire_bytes >= 16 << 30

@@ -620,7 +620,8 @@ int ws_launch_piece_scan_variant(const WsLaunch& L, u64 lo, u64 hi, unsigned cha
 // gfx950 (160 KiB per CU): 23,296 B and 27,136 B.
 WsOpt ws_piece_lds{0};
 WsOpt ws_piece_win{-1};  // "piece_win": log2 of the number of piece windows K2 streams side by side; -1 (default)
-                          // 2 for batches of >= 16 GiB the previous call advised as frames of one length, else 1
+                          // 2 for batches of >= 32 GiB, and of >= 16 GiB the previous call advised as frames of
+                          // one length, else 1
                           // (piece_wshift)
 
 int ws_piece_dyn_lds(const WsLaunch& L, u64 npieces, u32 g0) {
@@ -686,10 +687,16 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
 // paired over both placements, profiles/r05_win_ab.log) while cfg4 keeps the gain. So four windows
 // for batches of >= 1 M pieces (16 GiB) the previous call advised as frames of one length (g0, the
 // stride hint), two otherwise (first calls, captured calls, mixed lengths, smaller batches).
+// Round 6 (profiles/r06_win_rule_*.json, tools/exp_win_rule.py): first and
+// captured calls have no advice, so a 68.7 GB cfg4 round took two windows there and 21.7-22.0 ms
+// on its slow placement against 20.98-21.04 with four; four windows from the size alone also for
+// cfg3's 23.5 GB cost 0.6-0.9 % (captured and steady). So batches of >= 2 M pieces (32 GiB) take
+// four windows whatever the advice, 1-2 M pieces four only when advised as one frame length.
 #define PIECE_WIN4_MIN (1ull << 20)
+#define PIECE_WIN4_BIG (2ull << 20)
 static u32 piece_wshift(u64 npieces, u32 g0) {
     int pwin = ws_piece_win;
-    if (pwin < 0) pwin = g0 >= 2 && npieces >= PIECE_WIN4_MIN ? 2 : 1;
+    if (pwin < 0) pwin = npieces >= PIECE_WIN4_BIG || (g0 >= 2 && npieces >= PIECE_WIN4_MIN) ? 2 : 1;
     u32 wshift = (u32)(pwin > 6 ? 6 : pwin);
     while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
     return wshift;
