@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 run of bench.py into profiles/ (committed evidence).
 
     python tools/prof_summary.py gpurun_out/r01 r01 [--kernel ws_piece_unmask_kernel,ws_piece_walk_kernel]
+                                 [--launches-per-step N]
 
 The first --kernel name is the dominant kernel; traffic per step sums every listed kernel.
 
@@ -45,19 +46,34 @@ def per_launch(path, kernel, counter):
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
-def region_kernel_ms(src, names, kernel, warmup, steps):
+def region_kernel_ms(src, names, kernel, warmup, steps, lps=1):
+    """every listed kernel's dispatch time inside the bench's timed region, per step: from the end
+    of the dominant kernel's last warm-up dispatch to the end of its last timed one (lps: its
+    launches per step — the raw stream's split unmask launches twice)"""
     path = os.path.join(src, "trace", "run_kernel_trace.csv")
     if not os.path.exists(path) or steps <= 0:
         return None
     rows = list(csv.DictReader(open(path)))
     dom = sorted((r for r in rows if kernel in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
-    if len(dom) < warmup + steps:
+    if len(dom) < (warmup + steps) * lps:
         return None
-    t0 = int(dom[warmup - 1]["End_Timestamp"]) if warmup else 0
-    t1 = int(dom[warmup + steps - 1]["End_Timestamp"])
-    tot = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
-              if any(n in r["Kernel_Name"] for n in names) and t0 <= int(r["Start_Timestamp"]) < t1)
-    return tot / steps / 1e6
+    t0 = int(dom[warmup * lps - 1]["End_Timestamp"]) if warmup else 0
+    t1 = int(dom[(warmup + steps) * lps - 1]["End_Timestamp"])
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
+                if any(n in r["Kernel_Name"] for n in names) and t0 <= int(r["Start_Timestamp"]) < t1)
+    # the union of the dispatch intervals (kernels on a side stream overlap the call's own: the
+    # device is busy once for both)
+    busy, cur_s, cur_e = 0, None, None
+    for a, b in iv:
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    return busy / steps / 1e6
 
 
 def main():
@@ -65,6 +81,8 @@ def main():
     names = (sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv
              else "ws_piece_unmask_kernel,ws_piece_walk_kernel").split(",")
     kernel = names[0]
+    # launches of the dominant kernel per step (the raw stream's split unmask: 2)
+    lps = int(sys.argv[sys.argv.index("--launches-per-step") + 1]) if "--launches-per-step" in sys.argv else 1
     out = os.path.join(REPO, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, tag + "_kernel_stats.csv"))
@@ -81,13 +99,14 @@ def main():
         w, b = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), k, "WRITE_SIZE")
         per_kernel[k] = {"avg_ns": float(st[0]["AverageNs"]) if st else None, "calls": int(st[0]["Calls"]) if st else 0,
                          "fetch_kib": f, "write_kib": w, "fetch_factor": fetch_factor(k)}
+        m = lps if k == kernel else 1                   # per step
         if f is None or w is None:
             fetch_kib = write_kib = None
             fetch_corr = None
         elif fetch_kib is not None:
-            fetch_kib += f
-            write_kib += w
-            fetch_corr += fetch_factor(k) * f
+            fetch_kib += m * f
+            write_kib += m * w
+            fetch_corr += m * fetch_factor(k) * f
         if k == kernel:
             nf, nw = a, b
     bench = json.load(open(os.path.join(src, "bench.json")))
@@ -95,6 +114,7 @@ def main():
     algo = rf.get("algo_bytes_per_launch") or rf.get("algo_bytes_per_step")
     rec = {
         "kernel": stats[0]["Name"] if stats else kernel,
+        "launches_per_step": lps,
         "rocprof_calls": int(stats[0]["Calls"]) if stats else 0,
         "rocprof_avg_ns": float(stats[0]["AverageNs"]) if stats else None,
         "rocprof_min_ns": float(stats[0]["MinNs"]) if stats else None,
@@ -128,15 +148,16 @@ def main():
         if "per_kernel_ns_profiled" in rf:
             rf["per_kernel_ns_profiled"] = rec["per_kernel_avg_ns"]
     # consistency: the step's kernels against the bench line of the same traced process — a
-    # kernel cannot take longer than the step that contains it. rocprof's averages cover every
+    # kernel cannot take longer than the step that contains it (dispatches that overlap, on a
+    # side stream, count once: the union of their intervals). rocprof's averages cover every
     # dispatch of the process (warm-up calls too), so the check uses the dispatches inside the
     # timed region: from the end of the dominant kernel's last warm-up dispatch to the end of
     # its last timed one (kernel trace), every listed kernel's durations summed, / steps.
-    ks = [v["avg_ns"] for v in per_kernel.values() if v["avg_ns"] is not None]
+    ks = [v["avg_ns"] * (lps if k == kernel else 1) for k, v in per_kernel.items() if v["avg_ns"] is not None]
     rec["rocprof_kernel_sum_ms"] = round(sum(ks) / 1e6, 4) if ks else None
     step = bench.get("ms_per_step")
     rec["same_run_ms_per_step"] = step
-    region = region_kernel_ms(src, names, kernel, int(bench.get("warmup") or 0), int(bench.get("steps") or 0))
+    region = region_kernel_ms(src, names, kernel, int(bench.get("warmup") or 0), int(bench.get("steps") or 0), lps)
     rec["timed_region_kernel_ms_per_step"] = round(region, 4) if region is not None else None
     if bench.get("scaling") == "strong" and step:                  # cfg4: the step sums the rounds
         rounds = int(bench.get("config", {}).get("rounds_per_rank") or 1)
@@ -151,7 +172,8 @@ def main():
         v = region if region is not None else sum(ks) / 1e6
         rec["kernel_sum_le_step"] = v <= step
         rec["kernel_sum_frac_of_step"] = round(v / step, 4)
-        rec["check"] = ("kernels inside the timed region (kernel trace) <= the step" if region is not None
+        rec["check"] = ("kernels inside the timed region (kernel trace, union of their intervals) <= the step"
+                        if region is not None
                         else "rocprof averages <= the step")
     rec["bench_source"] = "the JSON line printed by the rocprofv3 --kernel-trace run itself (tools/profile.sh)"
     json.dump(rec, open(os.path.join(out, tag + "_pmc.json"), "w"), indent=1)
