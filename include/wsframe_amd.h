@@ -246,7 +246,7 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * beside it on a side stream in chunks of twice the largest chunk;
  * that walk starts after the plan 0, after the first part's owner walks 1 or its emit 2; the first
  * part's chunks are that chunk >> 0..6, default 2; "stream_side_prio": the side stream's priority, 0
- * default, 1 least (default), 2 greatest), "k2_timing" (see
+ * default (default), 1 least, 2 greatest), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);

@@ -1360,7 +1360,10 @@ WsOpt ws_stream_split{24};      // "stream_split": eager device-planned walks: K
                                 // of the pieces, the walk past them runs beside it on a side stream (0: no split)
 WsOpt ws_stream_split_wait{0};  // "stream_split_wait": part 1's walk starts after the plan (0), part 0's owner
                                 // walks (1) or part 0's emit (2)
-WsOpt ws_stream_side_prio{1};   // "stream_side_prio": the split walk's side stream priority: 0 default, 1 least, 2 greatest
+WsOpt ws_stream_side_prio{0};   // "stream_side_prio": the split walk's side stream priority: 0 default, 1 least, 2 greatest
+                                // (a stream of the least priority measured 7.82-7.85 ms against 7.91 on a fresh process,
+                                // but 8.24 against 7.61 after the host path's three pipeline streams: its walk then waited
+                                // for the first unmask launch; the greatest 10.14 — profiles/r06_stream_side_prio.log)
 WsOpt ws_stream_c0{2};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
