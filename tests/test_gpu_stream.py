@@ -447,8 +447,10 @@ def split_opts():
     """restores the split options after a test that changes them"""
     yield
     W.set_option("stream_split", 24)
+    W.set_option("stream_split2", 0)
     W.set_option("stream_split_wait", 0)
     W.set_option("stream_c0", 2)
+    W.set_option("stream_c1", 1)
     W.set_option("stream_rw", 1)
 
 
@@ -458,30 +460,38 @@ def _frames_before(wire, nbytes, mf=1 << 17):
     return int(np.searchsorted(fo, nbytes))
 
 
-@pytest.mark.parametrize("split,wait,c0", [(1, 0, 2), (16, 0, 2), (16, 1, 0), (16, 2, 6), (40, 0, 3), (128, 0, 2),
-                                           (255, 2, 2)])
-def test_stream_split_boundaries(dev, split_opts, split, wait, c0):
-    """the split point (piece p0 = npieces * split / 256) falls inside a frame; part 0 (small chunks)
-    hands the chain over to part 1 mid-frame; streams ending (max_frames, truncation, garbage, a
-    decode error) inside part 0, at the hand-off and inside part 1; two buffer phases. Every call
-    bit-exact vs the oracle and the split taken (stat stream_splits)"""
+@pytest.mark.parametrize("split,split2,wait,c0,c1", [(1, 0, 0, 2, 1), (16, 0, 0, 2, 1), (16, 0, 1, 0, 1),
+                                                    (16, 0, 2, 6, 1), (40, 0, 0, 3, 1), (128, 0, 0, 2, 1),
+                                                    (255, 0, 2, 2, 1), (8, 32, 0, 3, 1), (2, 5, 1, 6, 0),
+                                                    (24, 200, 2, 2, 3), (100, 101, 0, 0, 6)])
+def test_stream_split_boundaries(dev, split_opts, split, split2, wait, c0, c1):
+    """the split points (piece p0 = npieces * split / 256, and with split2 a second cut: three parts)
+    fall inside frames; each part (its own chunk size) hands the chain over to the next mid-frame;
+    streams ending (max_frames, truncation, garbage, a decode error) inside part 0, at the hand-off
+    and inside the later parts; two buffer phases. Every call bit-exact vs the oracle and the split
+    taken (stat stream_splits)"""
     W.set_option("stream_split", split)
+    W.set_option("stream_split2", split2)
     W.set_option("stream_split_wait", wait)
     W.set_option("stream_c0", c0)
-    rng = np.random.default_rng(600 + split)
+    W.set_option("stream_c1", c1)
+    rng = np.random.default_rng(600 + split + split2)
     wire = long_stream(rng, 40 << 20, mix3)
     x = len(wire) * split // 256
     n0 = W.get_stat("stream_splits")
     run(dev, wire, 1 << 16)
     run(dev, wire, 1 << 16, shift=7)
     assert W.get_stat("stream_splits") >= n0 + 2
-    # max_frames inside part 0, just past the split point and inside part 1
-    for at in (x // 2, x + 70000, (x + len(wire)) // 2):
+    # max_frames inside part 0, just past the split point and inside the later part(s)
+    x2 = len(wire) * split2 // 256 if split2 > split else len(wire)
+    for at in sorted({x // 2, x + 70000, (x + x2) // 2, x2 + 70000, (x2 + len(wire)) // 2}):
+        if at >= len(wire):
+            continue
         mf = max(1, _frames_before(wire, at))
         r = run(dev, wire, mf)
         assert int(r["n_frames"]) <= mf
-    # garbage and a LEN_WRAP header around the split point
-    for at in (max(0, x - 5000), x + 3, min(len(wire) - 64, x + (20 << 20) // 3)):
+    # garbage around the split points
+    for at in (max(0, x - 5000), x + 3, min(len(wire) - 64, x + (20 << 20) // 3), min(len(wire) - 64, x2 + 11)):
         g = wire.copy()
         g[at:at + 37] = rng.integers(0, 256, 37, dtype=np.uint8)
         run(dev, g, 1 << 16)

@@ -33,7 +33,8 @@ extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
-extern WsOpt ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio;
+extern WsOpt ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
+    ws_stream_c1;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips,
     ws_stat_stream_splits;
@@ -112,6 +113,14 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_split_wait")) {
         if (value < 0 || value > 2) return -1;
         ws_stream_split_wait = (int)value;
+    }
+    else if (!strcmp(name, "stream_split2")) {
+        if (value < 0 || value > 255) return -1;
+        ws_stream_split2 = (int)value;
+    }
+    else if (!strcmp(name, "stream_c1")) {
+        if (value < 0 || value > 6) return -1;
+        ws_stream_c1 = (int)value;
     }
     else if (!strcmp(name, "stream_side_prio")) {
         if (value < 0 || value > 2) return -1;
@@ -193,7 +202,7 @@ struct WsStreamWs {
                                    // record node), so a destroyed graph's replays are known to be finished
     hipStream_t side = nullptr;    // the raw stream's split walk: part 1 runs here (ws_stream.hip RwSplit)
     int side_prio = 0;             // ... created with this priority choice (0 default, 1 least, 2 greatest)
-    hipEvent_t sev[3] = {};        // ... and its fork / join events
+    hipEvent_t sev[WS_SIDE_EVENTS] = {};   // ... and its fork / join events
 };
 struct WsDevState {
     int init = 0;
@@ -540,7 +549,7 @@ int WsSlot::side(hipStream_t* side_out, hipEvent_t* ev, int prio) {
         if (e != hipSuccess) return ws_set_err("side stream (raw stream split)", e);
         w->side = nullptr;
     }
-    if (!w->side || !w->sev[2]) {
+    if (!w->side || !w->sev[WS_SIDE_EVENTS - 1]) {
         hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
         (void)hipThreadExchangeStreamCaptureMode(&m);
         int least = 0, greatest = 0;
@@ -552,13 +561,13 @@ int WsSlot::side(hipStream_t* side_out, hipEvent_t* ev, int prio) {
                          : hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
             w->side_prio = prio;
         }
-        for (int k = 0; k < 3 && e == hipSuccess; ++k)
+        for (int k = 0; k < WS_SIDE_EVENTS && e == hipSuccess; ++k)
             if (!w->sev[k]) e = hipEventCreateWithFlags(&w->sev[k], hipEventDisableTiming);
         (void)hipThreadExchangeStreamCaptureMode(&m);
         if (e != hipSuccess) return ws_set_err("side stream (raw stream split)", e);
     }
     *side_out = w->side;
-    for (int k = 0; k < 3; ++k) ev[k] = w->sev[k];
+    for (int k = 0; k < WS_SIDE_EVENTS; ++k) ev[k] = w->sev[k];
     return 0;
 }
 

@@ -407,7 +407,8 @@ int ws_device_info(int* cus, int* lds_per_cu);
 #define WS_AUX_HEAD 256
 // zeroed at allocation (and when a capture adopts a slot): the head and the 256 B after it, where
 // the raw stream's device walk keeps its plan (RwPlan::seen_max is read before its first write)
-#define WS_AUX_ZERO (WS_AUX_HEAD + 256)
+#define WS_AUX_ZERO (WS_AUX_HEAD + 512)
+#define WS_SIDE_EVENTS 4          // the raw stream's split walk: side start + one per part (RW_NP 3)
 struct WsAux {
     void* d;              // device scratch
     void* h;              // pinned host scratch (nullptr until requested)
@@ -429,7 +430,7 @@ struct WsSlot {
     int encode_workspace(size_t bytes, void** out);
     int aux(size_t dbytes, size_t hbytes, WsAux* out);
     int advice(int** host, int** dev);                             // the stride hint words (eager)
-    int side(hipStream_t* side, hipEvent_t* ev, int prio);         // the raw stream's split walk: side stream + 3 events
+    int side(hipStream_t* side, hipEvent_t* ev, int prio);         // the raw stream's split walk: side stream + events
 };
 bool ws_capturing(hipStream_t stream);
 int ws_launch_piece(const WsLaunch& L, u64 lo, u64 hi, unsigned char* ws, u32 gen, int* advice,

@@ -508,11 +508,12 @@ struct RwOwn {            // phase B: the walk from a window exit to the chunk's
 
 // The walk's geometry chosen on the device (captured calls: the host cannot read the sample):
 // R1-R3, the linker and the emit take it from here; scratch is sized for the caps at capture.
-// Round 6: the rest of the stream after the sample is one or two PARTS, each a chunk grid of
-// its own. With a split (stream_split), part 0 = [P, Pb) in small chunks (its owner walks are
-// short: it is the walk K2's first launch waits for) and part 1 = [Pb, len) in the usual
-// chunks; part 1's walk runs on a side stream beside K2 over part 0's pieces. Chunk arrays are
-// indexed by the global chunk g = cbase + local index; per-part lists start at their bases.
+// Round 6: the rest of the stream after the sample is one to RW_NP PARTS, each a chunk grid of
+// its own. With a split (stream_split), part 0 = [P, B1) in small chunks (its owner walks are
+// short: it is the walk K2's first launch waits for), the last part = [B_last, len) in large
+// chunks, and (stream_split2) a middle part; the parts after part 0 are walked on a side stream
+// beside K2's launches over the earlier parts' pieces. Chunk arrays are indexed by the global
+// chunk g = cbase + local index; per-part lists start at their bases.
 struct RwPart {
     u64 P;                // the part's chunk grid origin
     u64 C;                // its chunk bytes
@@ -520,18 +521,37 @@ struct RwPart {
     u32 stgn, pad;        // staging per owner
     u64 stg_base, cand_base;  // where its staging and candidate lists start (entries)
 };
+#define RW_NP 3           // parts of a split walk at most
 struct RwPlan {
-    RwPart pt[2];         // part 1 empty (n = 0) without a split
-    u32 nchunks;          // n0 + n1 (global chunk count)
+    RwPart pt[RW_NP];     // parts past nparts empty (n = 0)
+    u32 nchunks;          // sum of the parts' chunks (global chunk count)
     u32 need_mask, active, nf;   // nf: frames before pt[0].P
-    u32 nrows[2], linked[2];     // emit rows of each part (rows at tab[cbase + r]); linked: rows final
+    u32 nparts, seen_max; // seen_max: the longest frame the previous walk on this stream wrote (emit, linker)
+    u32 nrows[RW_NP], linked[RW_NP];   // emit rows of each part (rows at tab[cbase + r]); linked: rows final
     u64 sample_out[4];    // stream_walk's report of the sample / of a linked chunk walk
-    u32 seen_max;         // the longest frame the previous walk on this stream wrote (emit, linker)
-    u32 nw0;              // the item count K2's first launch reads: every item it may need is written
-    u64 h_ent;            // the hand-off from part 0 to part 1: the chain's entry, frames before it,
-    u32 h_nf, h_state;    // state 0 none yet, 1 part 1 continues at h_ent, 2 the walk ended in part 0
+    // the hand-off into part k (k >= 1): the chain's entry, the frames before it, and its state —
+    // 0 not yet, 1 part k continues at in_ent[k], 2 the walk ended before part k
+    u64 in_ent[RW_NP];
+    u32 in_nf[RW_NP], in_state[RW_NP];
+    u32 nw[RW_NP];        // the item count K2's launch k reads (k < nparts - 1): every item it may need is written
 };
-static_assert(sizeof(RwPlan) <= 256, "RwPlan lies in the zeroed aux range (WS_AUX_ZERO)");
+static_assert(sizeof(RwPlan) <= WS_AUX_ZERO - WS_AUX_HEAD, "RwPlan lies in the zeroed aux range (WS_AUX_ZERO)");
+
+// the walk ended in part `part` with `cnt` items: every later K2 launch reads the final count, every
+// later part is a no-op (one thread)
+__device__ __forceinline__ void rw_end_counts(RwPlan* plan, int part, u32 cnt) {
+    for (int k = part; k < RW_NP; ++k) plan->nw[k] = cnt;
+}
+__device__ __forceinline__ void rw_end_states(RwPlan* plan, int part) {
+    for (int k = part + 1; k < RW_NP; ++k) plan->in_state[k] = 2;
+}
+// part `part` hands the chain over to the next part at `ent` with `nf` frames before it (one thread)
+__device__ __forceinline__ void rw_hand_over(RwPlan* plan, int part, u64 ent, u32 nf) {
+    plan->in_ent[part + 1] = ent;
+    plan->in_nf[part + 1] = nf;
+    plan->nw[part] = nf;
+    plan->in_state[part + 1] = 1;
+}
 
 // a kernel's chunk grid: the plan's part (device-planned calls) or the host's arguments
 struct RwGeo {
@@ -808,7 +828,7 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
                                                         RwPlan* __restrict__ plan, int part) {
     u64 row = blockIdx.x, obase = 0, sbase = 0;
     if (plan) {                                                              // rows written by the linker
-        if (!plan->active || blockIdx.x >= plan->nrows[part] || (part == 1 && plan->h_state != 1)) return;
+        if (!plan->active || blockIdx.x >= plan->nrows[part] || (part >= 1 && plan->in_state[part] != 1)) return;
         const RwPart& pt = plan->pt[part];
         stgn = pt.stgn;
         row += pt.cbase;                                                     // the part's rows start at its first chunk
@@ -819,9 +839,9 @@ __global__ __launch_bounds__(64) void ws_rw_emit_kernel(const unsigned char* __r
     const u64 ent = t[0], exit_w = t[1], nf0 = t[2], cnt_w = t[3], oi = t[4], n_par = t[5], cs0 = t[7];
     const bool last = t[6] != 0;
     const u32 lane = threadIdx.x;
-    // the row that ends the walk in part 0 also writes the count K2's first launch reads
+    // the row that ends the walk also writes the count K2's launches from this part on read
     auto note_end = [&](const SwOut& o) {
-        if (plan && part == 0 && last && lane == 0) plan->nw0 = o.cnt;
+        if (plan && last && lane == 0) rw_end_counts(plan, part, o.cnt);
     };
     if (oi == ~0ull) {
         const SwOut o = stream_walk(buf, len, ent, 0, (u32)nf0, len, true, max_frames, desc, items, ptr, pend, nwork,
@@ -878,7 +898,8 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
                                                         u32x4* __restrict__ items, u64* __restrict__ ptr, u64 pend,
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int fresh, u64* __restrict__ seg, u32* __restrict__ disorder,
-                                                        SdMirror* __restrict__ mirror, u64 split_x, u32 c0_shift) {
+                                                        SdMirror* __restrict__ mirror, u64 split_x0, u64 split_x1,
+                                                        u32 c0_shift, u32 c1_shift) {
     const u32 lane = threadIdx.x;
     // the previous device walk's longest frame: 0 before the first (the plan lies in the WS_AUX_ZERO range,
     // zeroed when the aux buffer is allocated or a capture adopts the slot; the host-linked walk's
@@ -891,8 +912,8 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     auto finished = [&](u32 cnt) {
         if (lane == 0) {
             plan->active = 0;
-            plan->nw0 = cnt;
-            plan->h_state = 2;
+            rw_end_counts(plan, 0, cnt);
+            rw_end_states(plan, -1);
         }
     };
     if (!fresh && sd->phase == SD_DONE) {                                    // the passes finished it
@@ -937,58 +958,86 @@ __global__ __launch_bounds__(64) void ws_rw_plan_kernel(const unsigned char* __r
     }
     const u32 seenm = o.maxlen > seen ? o.maxlen : seen;
     u64 C = rw_pow2_clamp(mean * 1024, cmin > RW_CMIN ? cmin : RW_CMIN, cmin > cmax ? cmin : cmax);
-    // split (split_x: the first byte K2's second launch owns): part 0 = [P1, Pb >= split_x) in
-    // chunks of C >> c0_shift, at least twice the window a frame start needs (its owner walks are
-    // the latency K2's first launch waits for), part 1 = [Pb, len) in chunks of C
-    const bool split = split_x > P1 && split_x < len;
+    // split (split_x0 / split_x1: the first bytes K2's second / third launch own; 0 = none): part k
+    // ends at the first chunk start at or past split_x_k; part 0's chunks are C >> c0_shift, a middle
+    // part's C >> c1_shift (at least twice the window a frame start needs), the last part's C
     const u64 hneed = rw_window(mean, seenm, 4 * (u64)RW_HMAX);
-    u64 C0 = C, n0 = 0, n1 = 0, Pb = len;
+    const u64 xs[RW_NP - 1] = {split_x0, split_x1};
+    const u32 shifts[RW_NP - 1] = {c0_shift, c1_shift};
+    u64 Pk[RW_NP], Ck[RW_NP], nk[RW_NP];
+    u32 np = 1;
     for (;;) {
-        if (split) {
-            C0 = rw_pow2_clamp((C >> c0_shift) > 2 * hneed ? (C >> c0_shift) : 2 * hneed, RW_CMIN, C);
-            n0 = (split_x - P1 + C0 - 1) / C0;
-            Pb = P1 + n0 * C0;
-            if (Pb >= len) { Pb = len; n0 = (len - P1 + C0 - 1) / C0; }
-            n1 = Pb < len ? (len - Pb + C - 1) / C : 0;
-        } else {
-            C0 = C;
-            n0 = (len - P1 + C - 1) / C;
+        u64 B = P1, tot = 0;
+        np = 0;
+        for (u32 k = 0; k < RW_NP; ++k) {
+            const bool lastp = k + 1 == RW_NP || !xs[k] || xs[k] >= len;
+            u64 Cx = C;
+            if (!lastp) {
+                const u64 want = (C >> shifts[k]) > 2 * hneed ? (C >> shifts[k]) : 2 * hneed;
+                Cx = rw_pow2_clamp(want, RW_CMIN, C);
+            }
+            u64 E = len;
+            if (!lastp) {
+                E = xs[k] > B ? B + (xs[k] - B + Cx - 1) / Cx * Cx : B;
+                if (E >= len) E = len;
+            }
+            Pk[k] = B; Ck[k] = Cx; nk[k] = E > B ? (E - B + Cx - 1) / Cx : 0;
+            tot += nk[k];
+            ++np;
+            B = E;
+            if (lastp || E >= len) break;
         }
-        const u64 nch = n0 + n1;
         // fit the caps (cmin makes the chunk count fit; the smallest staging and candidate lists too)
-        if (nch <= nchunks_cap && nch * RW_D * 64 <= stg_cap && nch * 64 <= cand_cap) break;
+        if (tot <= nchunks_cap && tot * RW_D * 64 <= stg_cap && tot * 64 <= cand_cap) break;
         C <<= 1;
     }
-    const u32 H0 = rw_window(mean, seenm, C0), H1 = rw_window(mean, seenm, C);
-    u64 stg0 = rw_pow2_clamp(2 * C0 / (mean ? mean : 1), 256, RW_CAP_STGN);
-    u64 stg1 = rw_pow2_clamp(2 * C / (mean ? mean : 1), 256, RW_CAP_STGN);
-    while ((stg0 > 64 || stg1 > 64) && (n0 * stg0 + n1 * stg1) * RW_D > stg_cap) {
-        stg0 = stg0 > 64 ? stg0 >> 1 : stg0;
-        stg1 = stg1 > 64 ? stg1 >> 1 : stg1;
+    u64 Hk[RW_NP], stgk[RW_NP], capk[RW_NP];
+    u64 stg_need = 0, cand_need = 0;
+    for (u32 k = 0; k < np; ++k) {
+        Hk[k] = rw_window(mean, seenm, Ck[k]);
+        stgk[k] = rw_pow2_clamp(2 * Ck[k] / (mean ? mean : 1), 256, RW_CAP_STGN);
+        capk[k] = Hk[k] / 32;
     }
-    u64 cap0 = H0 / 32, cap1 = H1 / 32;
-    while ((cap0 > 64 || cap1 > 64) && n0 * cap0 + n1 * cap1 > cand_cap) {
-        cap0 = cap0 > 64 ? cap0 >> 1 : cap0;
-        cap1 = cap1 > 64 ? cap1 >> 1 : cap1;
+    for (;;) {                                                               // shrink staging / candidates to the caps
+        stg_need = cand_need = 0;
+        bool can = false;
+        for (u32 k = 0; k < np; ++k) {
+            stg_need += nk[k] * RW_D * stgk[k];
+            cand_need += nk[k] * capk[k];
+            can = can || stgk[k] > 64 || capk[k] > 64;
+        }
+        if ((stg_need <= stg_cap && cand_need <= cand_cap) || !can) break;
+        for (u32 k = 0; k < np; ++k) {
+            if (stg_need > stg_cap && stgk[k] > 64) stgk[k] >>= 1;
+            if (cand_need > cand_cap && capk[k] > 64) capk[k] >>= 1;
+        }
     }
     if (lane == 0) {
-        RwPart& a = plan->pt[0];
-        a.P = P1; a.C = C0; a.H = H0; a.n = (u32)n0; a.cbase = 0; a.capc = (u32)cap0; a.stgn = (u32)stg0;
-        a.stg_base = 0; a.cand_base = 0;
-        RwPart& b = plan->pt[1];
-        b.P = Pb; b.C = C; b.H = H1; b.n = (u32)n1; b.cbase = (u32)n0; b.capc = (u32)cap1; b.stgn = (u32)stg1;
-        b.stg_base = n0 * RW_D * stg0; b.cand_base = n0 * cap0;
-        plan->nchunks = (u32)(n0 + n1);
+        u64 cb = 0, sb = 0, cdb = 0;
+        for (u32 k = 0; k < RW_NP; ++k) {
+            RwPart& t = plan->pt[k];
+            if (k < np) {
+                t.P = Pk[k]; t.C = Ck[k]; t.H = (u32)Hk[k]; t.n = (u32)nk[k]; t.cbase = (u32)cb; t.capc = (u32)capk[k];
+                t.stgn = (u32)stgk[k]; t.stg_base = sb; t.cand_base = cdb;
+                cb += nk[k]; sb += nk[k] * RW_D * stgk[k]; cdb += nk[k] * capk[k];
+            } else {
+                t.P = len; t.C = C; t.H = RW_HMIN; t.n = 0; t.cbase = (u32)cb; t.capc = 64; t.stgn = 64;
+                t.stg_base = sb; t.cand_base = cdb;
+            }
+            plan->nrows[k] = 0;
+            plan->linked[k] = 0;
+            plan->in_ent[k] = 0;
+            plan->in_nf[k] = 0;
+            plan->in_state[k] = 0;
+            plan->nw[k] = 0;
+        }
+        plan->nchunks = (u32)cb;
+        plan->nparts = np;
         plan->need_mask = (buf[P1 + 1] & 0x80u) ? 1u : 0u;                   // client frames: masked
         plan->nf = o.nf;
-        plan->nrows[0] = plan->nrows[1] = 0;
-        plan->linked[0] = plan->linked[1] = 0;
-        plan->nw0 = 0;
-        plan->h_ent = 0;
-        plan->h_nf = 0;
-        plan->h_state = 0;
         plan->seen_max = 0;                 // this call's emit and linker fill it in
         plan->active = 1;
+        rw_end_states(plan, (int)np - 1);   // parts past the last one are no-ops
     }
 }
 
@@ -1015,22 +1064,22 @@ __global__ __launch_bounds__(64) void ws_rw_plink_kernel(u64 len, const RwPlan* 
                                                          const RwOwn* __restrict__ own, RwLink* __restrict__ lk,
                                                          int part) {
     const u32 lane = threadIdx.x, cl = blockIdx.x;                           // local chunk
-    if (!plan->active || cl >= plan->pt[part].n || (part == 1 && plan->h_state != 1)) return;
+    if (!plan->active || cl >= plan->pt[part].n || (part >= 1 && plan->in_state[part] != 1)) return;
     const RwPart& pt = plan->pt[part];
     const u64 P = pt.P, C = pt.C;
     const u32 H = pt.H, nchunks = plan->nchunks;
     const u64 c = (u64)pt.cbase + cl;                                        // global chunk
     const u64 cs0 = P + (u64)cl * C;
     const bool lastc = c + 1 == nchunks;
-    // the next chunk's size (part 0's last chunk: part 1's first)
-    const u64 Cn = (part == 0 && cl + 1 == pt.n && plan->pt[1].n) ? plan->pt[1].C : C;
+    // the next chunk's size (a part's last chunk: the next part's first)
+    const u64 Cn = (cl + 1 == pt.n && part + 1 < (int)plan->nparts) ? plan->pt[part + 1].C : C;
     auto rl64 = [](u64 v, int i) -> u64 {
         return (u64)(u32)__builtin_amdgcn_readlane((int)(u32)v, i) |
                ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), i) << 32);
     };
     // the entry: the common exit of chunk c-1's live owners; a part's first chunk: the part's
-    // origin (part 0) or part 0's hand-off (part 1, the chain's exact entry)
-    u64 ent = part == 0 ? P : plan->h_ent;
+    // origin (part 0) or the previous part's hand-off (the chain's exact entry)
+    u64 ent = part == 0 ? P : plan->in_ent[part];
     bool ok = true;
     if (cl) {
         const u64 oi = (c - 1) * RW_D + (lane & (RW_D - 1));
@@ -1114,12 +1163,12 @@ __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, Rw
     __shared__ u64 s_wsum[RW_PS_T / 64];
     __shared__ u64 s_carry;
     const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (!plan->active || (part == 1 && plan->h_state != 1)) return;
+    if (!plan->active || (part >= 1 && plan->in_state[part] != 1)) return;
     const RwPart& pt = plan->pt[part];
     const u32 n = pt.n, cb = pt.cbase, stgn = pt.stgn;
-    // part 0 of a split hands the chain over to part 1 when no chunk of it ends the walk
-    const bool has_next = part == 0 && plan->pt[1].n != 0;
-    if (tid == 0) { s_stop = n; s_bad = 0; s_carry = part == 0 ? plan->nf : plan->h_nf; }
+    // a part of a split hands the chain over to the next part when no chunk of it ends the walk
+    const bool has_next = part + 1 < (int)plan->nparts;
+    if (tid == 0) { s_stop = n; s_bad = 0; s_carry = part == 0 ? plan->nf : plan->in_nf[part]; }
     __syncthreads();
     // the first chunk that is invalid or ends the chain
     for (u32 c = tid; c < n; c += RW_PS_T) {
@@ -1171,14 +1220,10 @@ __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, Rw
     if (tid == 0 && !s_bad) {
         if (stop < n) {                                                      // the walk ends in this part
             plan->nrows[part] = stop + 1;
-            if (part == 0) plan->h_state = 2;                                // (nw0: the last row's emit)
-        } else {                                                             // part 0 hands over
-            plan->nrows[0] = n;
-            const u64 ent = n ? own[lk[cb + n - 1].oi].exit : pt.P;
-            plan->h_ent = ent;
-            plan->h_nf = (u32)s_carry;
-            plan->nw0 = (u32)s_carry;
-            plan->h_state = 1;
+            rw_end_states(plan, part);                                       // (counts: the last row's emit)
+        } else {                                                             // this part hands over
+            plan->nrows[part] = n;
+            rw_hand_over(plan, part, n ? own[lk[cb + n - 1].oi].exit : pt.P, (u32)s_carry);
         }
         plan->linked[part] = 1;
     }
@@ -1200,15 +1245,15 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
                                                         u32* __restrict__ nwork, WebsocketSegResult_t* __restrict__ res,
                                                         int part) {
     const u32 lane = threadIdx.x;
-    if (!plan->active || plan->linked[part] || (part == 1 && plan->h_state != 1)) return;   // linked by pscan
+    if (!plan->active || plan->linked[part] || (part >= 1 && plan->in_state[part] != 1)) return;   // linked by pscan
     const RwPart& pt = plan->pt[part];
     const u64 P = pt.P, C = pt.C;
     const u32 H = pt.H, nchunks = plan->nchunks, stgn = pt.stgn, np = pt.n, cb = pt.cbase;
-    // part 0 of a split stops where part 1 begins and hands the chain over
-    const bool has_next = part == 0 && plan->pt[1].n != 0;
-    const u64 Pb = plan->pt[1].P;
-    u64 ent = part == 0 ? P : plan->h_ent;
-    u32 nfc = part == 0 ? plan->nf : plan->h_nf, rows = 0;
+    // a part of a split stops where the next part begins and hands the chain over
+    const bool has_next = part + 1 < (int)plan->nparts;
+    const u64 Pb = has_next ? plan->pt[part + 1].P : len;
+    u64 ent = part == 0 ? P : plan->in_ent[part];
+    u32 nfc = part == 0 ? plan->nf : plan->in_nf[part], rows = 0;
     bool last = false;
     u32 cnt_end = 0;                                                         // the count a finishing walk wrote
     bool ended_walk = false;
@@ -1335,16 +1380,11 @@ __global__ __launch_bounds__(64) void ws_rw_link_kernel(const unsigned char* __r
     rw_note_max(plan, mx, lane);
     if (lane == 0) {
         plan->nrows[part] = rows;
-        if (part == 0) {
-            if (handoff) {
-                plan->h_ent = ent;
-                plan->h_nf = nfc;
-                plan->nw0 = nfc;
-                plan->h_state = 1;
-            } else {
-                plan->h_state = 2;
-                if (ended_walk) plan->nw0 = cnt_end;                         // (else: the last row's emit writes it)
-            }
+        if (handoff) {
+            rw_hand_over(plan, part, ent, nfc);
+        } else {
+            rw_end_states(plan, part);
+            if (ended_walk) rw_end_counts(plan, part, cnt_end);              // (else: the last row's emit writes them)
         }
         plan->linked[part] = 1;
     }
@@ -1364,6 +1404,9 @@ WsOpt ws_stream_side_prio{0};   // "stream_side_prio": the split walk's side str
                                 // (a stream of the least priority measured 7.82-7.85 ms against 7.91 on a fresh process,
                                 // but 8.24 against 7.61 after the host path's three pipeline streams: its walk then waited
                                 // for the first unmask launch; the greatest 10.14 — profiles/r06_stream_side_prio.log)
+WsOpt ws_stream_split2{0};      // "stream_split2": a third part — K2's second launch ends at this many 256ths of the
+                                // pieces (> stream_split; 0: two parts)
+WsOpt ws_stream_c1{1};          // "stream_c1": a middle part's chunks are the last part's chunk >> this
 WsOpt ws_stream_c0{2};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
@@ -1588,17 +1631,19 @@ static RwDevLayout rw_dev_layout(u64 len) {
     return L;
 }
 
-// The split of a device-planned walk (round 6): K2 runs as two launches, over
-// the pieces before and after piece p0, and the walk of the stream past them (part 1) runs on a
-// side stream while the first launch streams. Side-stream work joins the caller's stream through
-// events (eager and captured calls alike: in a capture the events are the graph's fork and join).
+// The split of a device-planned walk (round 6): K2 runs as one launch per
+// part (pieces [0, p[0]), [p[0], p[1]), ..., [p[last], npieces)), and the walk of each part after
+// part 0 runs on a side stream while the earlier launches stream. Side-stream work joins the
+// caller's stream through events (a capture would fork and join through them too; captured calls
+// do not split, see the entry point).
 struct RwSplit {
-    u64 p0 = 0;                  // K2's first launch: pieces [0, p0); 0 = no split
-    u64 x = 0;                   // the first stream byte the second launch owns (piece p0's start)
+    u32 ncut = 0;                // K2 cut points (parts - 1); 0 = no split
+    u64 p[RW_NP - 1] = {};       // the cuts (pieces)
+    u64 x[RW_NP - 1] = {};       // the first stream byte of the piece at each cut
     hipStream_t side = nullptr;
-    hipEvent_t ev[3] = {};       // part-1 start, part 0 linked + emitted, part 1 emitted
+    hipEvent_t ev[RW_NP + 1] = {};   // side start, part 0 done, part 1 done, ...
     int wait = 0;                // part 1's R1-R3 start after: 0 the plan, 1 part 0's R3, 2 part 0's emit
-    u32 c0_shift = 2;            // part 0's chunks: C >> c0_shift (at least twice the window)
+    u32 shift[RW_NP - 1] = {2, 1};   // part 0's / a middle part's chunks: C >> shift
 };
 
 static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, WebsocketFrameDesc_t* d_desc,
@@ -1615,16 +1660,17 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     u64* cand = reinterpret_cast<u64*>(w + L.o_cand);
     RwLink* lk = reinterpret_cast<RwLink*>(w + L.o_lk);
     const int cmax_log = ws_stream_rw_cmax;                                  // one read per call
-    const bool split = sp && sp->p0;
-    // a split walk's part 1 runs beside K2: chunks twice the usual largest (fewer windows for R1 to
-    // scan beside the stream; its longer owner walks are hidden), part 0 = that >> c0_shift
+    const bool split = sp && sp->ncut;
+    // a split walk's last part runs beside K2: chunks twice the usual largest (fewer windows for R1 to
+    // scan beside the stream; its longer owner walks are hidden), the earlier parts' that >> shift
     const u64 cmax = std::min<u64>((cmax_log >= 16 && cmax_log <= 26 ? 1ull << cmax_log : RW_CMAX) << (split ? 1 : 0),
                                    RW_CMAX);
     hipError_t e = hipMemsetAsync(nrec, 0, L.zero_bytes, st);
     if (e != hipSuccess) return ws_set_err("hipMemsetAsync(stream walk counters)", e);
     hipLaunchKernelGGL(ws_rw_plan_kernel, dim3(1), dim3(64), 0, st, d_buf, len, max_frames, sd, plan, L.cmin, cmax,
                        (u32)L.nch_cap, L.cand_cap, L.stg_cap, d_desc, Pw.items, Pw.ptr, Pw.npieces, Pw.nwork, d_res,
-                       fresh, d_seg, Pw.disorder, mirror, split ? sp->x : 0ull, split ? sp->c0_shift : 0u);
+                       fresh, d_seg, Pw.disorder, mirror, split ? sp->x[0] : 0ull, split && sp->ncut > 1 ? sp->x[1] : 0ull,
+                       split ? sp->shift[0] : 0u, split ? sp->shift[1] : 0u);
     // one part's candidate, window and owner walks; its linking and emit
     auto rwalk = [&](hipStream_t s, int part) {
         // R1 and R2 grid-stride, R3 one lane per (chunk, exit): grids for the caps
@@ -1675,32 +1721,42 @@ static int rw_walk_device(unsigned char* d_buf, u64 len, u32 max_frames, Websock
     if (sp->wait >= 2) rwalk(sp->side, 1);
     rlink(sp->side, 1);
     RW_TRY(hipEventRecord(sp->ev[2], sp->side), "hipEventRecord(stream split)");
+    for (u32 k = 2; k <= sp->ncut; ++k) {                                    // later parts, one after the other
+        rwalk(sp->side, (int)k);
+        rlink(sp->side, (int)k);
+        RW_TRY(hipEventRecord(sp->ev[k + 1], sp->side), "hipEventRecord(stream split)");
+    }
 #undef RW_TRY
     if ((e = hipGetLastError()) != hipSuccess) return ws_set_err("stream walk (device) launch", e);
     return 0;
 }
 
-// K2 after a device-planned walk: one launch, or (split) the pieces before p0 with the count
-// part 0 left in the plan, then — once part 1 is emitted — the pieces from p0 on
+// K2 after a device-planned walk: one launch, or (split) one launch per part's pieces — launch k
+// (pieces [p[k-1], p[k])) with the item count part k left in the plan, once part k is emitted; the
+// last launch with the stream's final count
 std::atomic<unsigned long long> ws_stat_stream_splits{0};   // raw-stream calls whose K2 ran split (since load)
 static int rw_unmask(const WsLaunch& L, const PieceWs& Pw, u32 gen, const RwSplit* sp, const RwPlan* plan) {
-    if (!sp || !sp->p0) return ws_launch_piece_unmask(L, Pw, gen);
+    if (!sp || !sp->ncut) return ws_launch_piece_unmask(L, Pw, gen);
     ++ws_stat_stream_splits;
     const u64 cpp = 1ull << (PIECE_SHIFT_S - 4);                             // 16-B chunks per piece
-    PieceWs A = Pw;
-    A.npieces = sp->p0;
-    A.c_hi = std::min<u64>(Pw.c_hi, sp->p0 * cpp);
-    A.nwork = const_cast<u32*>(&plan->nw0);
-    int rc = ws_launch_piece_unmask(L, A, gen);
-    if (rc) return rc;
-    hipError_t e = hipStreamWaitEvent(L.stream, sp->ev[2], 0);
-    if (e != hipSuccess) return ws_set_err("hipStreamWaitEvent(stream split join)", e);
-    PieceWs B = Pw;
-    B.ptr = Pw.ptr + sp->p0;
-    B.pbase = Pw.pbase + sp->p0;
-    B.npieces = Pw.npieces - sp->p0;
-    B.c_lo = std::max<u64>(Pw.c_lo, sp->p0 * cpp);
-    return ws_launch_piece_unmask(L, B, gen);
+    for (u32 k = 0; k <= sp->ncut; ++k) {
+        const u64 a = k ? sp->p[k - 1] : 0, b = k < sp->ncut ? sp->p[k] : Pw.npieces;
+        if (k) {
+            hipError_t e = hipStreamWaitEvent(L.stream, sp->ev[k + 1], 0);
+            if (e != hipSuccess) return ws_set_err("hipStreamWaitEvent(stream split join)", e);
+        }
+        if (b <= a) continue;
+        PieceWs A = Pw;
+        A.ptr = Pw.ptr + a;
+        A.pbase = Pw.pbase + a;
+        A.npieces = b - a;
+        A.c_lo = std::max<u64>(Pw.c_lo, a * cpp);
+        A.c_hi = k < sp->ncut ? std::min<u64>(Pw.c_hi, b * cpp) : Pw.c_hi;
+        if (k < sp->ncut) A.nwork = const_cast<u32*>(&plan->nw[k]);
+        const int rc = ws_launch_piece_unmask(L, A, gen);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char* d_buf, unsigned long long len,
@@ -1795,14 +1851,20 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     // (eager calls only: a captured graph's branches are not run concurrently — the split measured
     // 8.57-8.59 ms against 8.06-8.08 unsplit for cfg3 replays, profiles/r06_stream_split_ab.log)
     if (dev_layout && !capture) {
-        const int spl = ws_stream_split, sw = ws_stream_split_wait, c0 = ws_stream_c0;   // one read each
-        const int pr = ws_stream_side_prio;
-        if (spl > 0 && spl < 256 && Pw.npieces >= 2) {
-            SP.p0 = std::max<u64>(1, Pw.npieces * (u64)spl / 256);
+        const int spl = ws_stream_split, spl2 = ws_stream_split2, sw = ws_stream_split_wait;   // one read each
+        const int c0 = ws_stream_c0, c1 = ws_stream_c1, pr = ws_stream_side_prio;
+        if (spl > 0 && spl < 256 && Pw.npieces >= 3) {
             const u64 lead0 = reinterpret_cast<uintptr_t>(d_buf) & 15;
-            SP.x = (SP.p0 << PIECE_SHIFT_S) - lead0;
+            SP.p[0] = std::max<u64>(1, Pw.npieces * (u64)spl / 256);
+            SP.ncut = 1;
+            if (spl2 > spl && spl2 < 256) {
+                const u64 p1 = Pw.npieces * (u64)spl2 / 256;
+                if (p1 > SP.p[0] && p1 < Pw.npieces) SP.p[SP.ncut++] = p1;
+            }
+            for (u32 k = 0; k < SP.ncut; ++k) SP.x[k] = (SP.p[k] << PIECE_SHIFT_S) - lead0;
             SP.wait = sw >= 0 && sw <= 2 ? sw : 0;
-            SP.c0_shift = c0 >= 0 && c0 <= 6 ? (u32)c0 : 2u;
+            SP.shift[0] = c0 >= 0 && c0 <= 6 ? (u32)c0 : 2u;
+            SP.shift[1] = c1 >= 0 && c1 <= 6 ? (u32)c1 : 1u;
             if ((rc = slot.side(&SP.side, SP.ev, pr >= 0 && pr <= 2 ? pr : 0))) return rc;
         }
     }
