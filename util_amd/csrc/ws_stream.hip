@@ -1223,7 +1223,9 @@ __global__ __launch_bounds__(RW_PS_T) void ws_rw_pscan_kernel(u32 max_frames, Rw
             rw_end_states(plan, part);                                       // (counts: the last row's emit)
         } else {                                                             // this part hands over
             plan->nrows[part] = n;
-            rw_hand_over(plan, part, n ? own[lk[cb + n - 1].oi].exit : pt.P, (u32)s_carry);
+            // (an empty part passes its own entry on: the plan's P for part 0, the hand-off into it else)
+            rw_hand_over(plan, part, n ? own[lk[cb + n - 1].oi].exit : (part == 0 ? pt.P : plan->in_ent[part]),
+                         (u32)s_carry);
         }
         plan->linked[part] = 1;
     }
