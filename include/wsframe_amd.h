@@ -242,11 +242,12 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * log2 of its largest chunk 16..26, pass rounds of a captured call 1..64, a captured
  * call's chunk records linked in parallel 0/1), "stream_split" / "stream_split2" / "stream_split_wait" /
  * "stream_c0" / "stream_c1" / "stream_side_prio" (raw stream, eager device-planned walk: the unmask's first launch takes this
- * many 256ths of the pieces, 0..255, default 24, 0 = one launch, while the walk of the stream past them runs
- * beside it on a side stream in chunks of twice the largest chunk;
+ * many 256ths of the pieces, 0..255, default 8, 0 = one launch, while the walk of the stream past them runs
+ * beside it on a side stream, its last part in chunks of twice the largest chunk;
  * that walk starts after the plan 0, after the first part's owner walks 1 or its emit 2; the first
- * part's chunks are that chunk >> 0..6, default 2; "stream_split2": 0 (default) or a second cut in 256ths
- * of the pieces past "stream_split" — a middle part, in chunks of that chunk >> "stream_c1" (default 1); "stream_side_prio": the side stream's priority, 0
+ * part's chunks are that chunk >> 0..6, default 3; "stream_split2": a second cut in 256ths of the pieces
+ * past "stream_split", default 48, 0 = two parts — a middle part, in chunks of that chunk >> "stream_c1"
+ * (default 2); "stream_side_prio": the side stream's priority, 0
  * default (default), 1 least, 2 greatest), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */

@@ -21,8 +21,8 @@ torch = pytest.importorskip("torch")
 
 DEFAULTS = {"path": -1, "scan_alpha": 1, "host_chunk_mb": 64, "piece_lds": 0,
             "piece_win": -1, "seg_win": 1, "reasm_path": 0, "reasm_cfg": 0, "enc_front": 1, "stream_rw": 1,
-            "stream_rw_cmax": 22, "stream_rounds": 4, "stream_plink": 1, "stream_split": 24, "stream_split_wait": 0,
-            "stream_c0": 2, "stream_side_prio": 0, "stream_split2": 0, "stream_c1": 1, "k2_timing": 0}
+            "stream_rw_cmax": 22, "stream_rounds": 4, "stream_plink": 1, "stream_split": 8, "stream_split_wait": 0,
+            "stream_c0": 3, "stream_side_prio": 0, "stream_split2": 48, "stream_c1": 2, "k2_timing": 0}
 
 VALUES = {"path": [-1, 1, 3, 4], "scan_alpha": [0, 1],
           "host_chunk_mb": [1, 64], "piece_lds": [0, 1, 56000], "piece_win": [-1, 0, 1, 2, 3, 4, 5, 6],

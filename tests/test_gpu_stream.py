@@ -446,11 +446,11 @@ def test_two_raw_streams_in_parallel_threads(dev):
 def split_opts():
     """restores the split options after a test that changes them"""
     yield
-    W.set_option("stream_split", 24)
-    W.set_option("stream_split2", 0)
+    W.set_option("stream_split", 8)
+    W.set_option("stream_split2", 48)
     W.set_option("stream_split_wait", 0)
-    W.set_option("stream_c0", 2)
-    W.set_option("stream_c1", 1)
+    W.set_option("stream_c0", 3)
+    W.set_option("stream_c1", 2)
     W.set_option("stream_rw", 1)
 
 

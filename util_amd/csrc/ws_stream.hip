@@ -1398,7 +1398,7 @@ WsOpt ws_stream_rw_cmax{22};    // "stream_rw_cmax": log2 of the largest chunk (
                                 // against 8.19-8.21 at 8 MiB and 8.14-8.15 at 2 MiB, profiles/r04_stream_cmax_ab.log)
 WsOpt ws_stream_rounds{4};      // "stream_rounds": pass rounds (A + B) enqueued per state read
 WsOpt ws_stream_plink{1};       // "stream_plink": captured calls link the chunk records in parallel (0: serial only)
-WsOpt ws_stream_split{24};      // "stream_split": eager device-planned walks: K2's first launch takes this many 256ths
+WsOpt ws_stream_split{8};       // "stream_split": eager device-planned walks: K2's first launch takes this many 256ths
                                 // of the pieces, the walk past them runs beside it on a side stream (0: no split)
 WsOpt ws_stream_split_wait{0};  // "stream_split_wait": part 1's walk starts after the plan (0), part 0's owner
                                 // walks (1) or part 0's emit (2)
@@ -1406,10 +1406,12 @@ WsOpt ws_stream_side_prio{0};   // "stream_side_prio": the split walk's side str
                                 // (a stream of the least priority measured 7.82-7.85 ms against 7.91 on a fresh process,
                                 // but 8.24 against 7.61 after the host path's three pipeline streams: its walk then waited
                                 // for the first unmask launch; the greatest 10.14 — profiles/r06_stream_side_prio.log)
-WsOpt ws_stream_split2{0};      // "stream_split2": a third part — K2's second launch ends at this many 256ths of the
-                                // pieces (> stream_split; 0: two parts)
-WsOpt ws_stream_c1{1};          // "stream_c1": a middle part's chunks are the last part's chunk >> this
-WsOpt ws_stream_c0{2};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
+WsOpt ws_stream_split2{48};     // "stream_split2": a third part — K2's second launch ends at this many 256ths of the
+                                // pieces (> stream_split; 0: two parts). Three parts 8 / 48 with part 0 in chunks of
+                                // C / 8 and the middle in C / 4: 7.53-7.56 ms against 7.57-7.59 for two parts 24 in
+                                // C / 4 (cfg3, profiles/r06_stream_split_ab.log)
+WsOpt ws_stream_c1{2};          // "stream_c1": a middle part's chunks are the last part's chunk >> this
+WsOpt ws_stream_c0{3};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
 std::atomic<unsigned long long> ws_stat_stream_skips{0};    // eager calls that skipped the pass rounds (since load)
 std::atomic<unsigned long long> ws_stat_rw_chunk_walks{0};  // chunks walked by one wavefront without a record
