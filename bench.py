@@ -22,6 +22,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import re
 import sys
 import threading
 import time
@@ -105,9 +106,13 @@ def pmc_traffic(kernel, algo_bytes, metric, graph=None):
         if kernel in rec.get("kernel", "") and rec.get("algo_bytes_per_launch") == algo_bytes \
                 and rec.get("bench_metric") == metric and rec.get("traffic_bytes_per_launch") \
                 and (graph is None or bool(g) == bool(graph)):
-            if best is None or os.path.getmtime(f) > os.path.getmtime(best[0]):
-                best = (f, rec)
-    return best
+            # newest = the highest round in the file name (r06_…), then the latest in-file time:
+            # file mtimes are the checkout's, not the profile's
+            m = re.match(r"r(\d+)_", os.path.basename(f))
+            key = (int(m.group(1)) if m else -1, str(rec.get("created") or ""), os.path.basename(f))
+            if best is None or key > best[2]:
+                best = (f, rec, key)
+    return best[:2] if best else None
 
 
 class Workload:

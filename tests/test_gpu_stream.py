@@ -451,6 +451,7 @@ def split_opts():
     W.set_option("stream_split_wait", 0)
     W.set_option("stream_c0", 3)
     W.set_option("stream_c1", 2)
+    W.set_option("stream_split_capture", 1)
     W.set_option("stream_rw", 1)
 
 
@@ -511,11 +512,14 @@ def test_stream_split_long_frames_and_host_path(dev, split_opts):
     run(dev, wire2, 1 << 16)
 
 
-def test_stream_split_captured(dev, split_opts):
-    """a captured raw-stream decode with the split option set: captured calls do not split (a
-    graph's branches run one after the other), replays of changing bytes and a max_frames stop
-    where part 0 would end are bit-exact each time"""
+@pytest.mark.parametrize("cap", [0, 1])
+def test_stream_split_captured(dev, split_opts, cap):
+    """a captured raw-stream decode with the split option set: with stream_split_capture (the
+    default) the side stream becomes a graph branch, without it the captured call takes one
+    launch. Replays of changing bytes and a max_frames stop where part 0 would end
+    are bit-exact each time"""
     W.set_option("stream_split", 32)
+    W.set_option("stream_split_capture", cap)
     rng = np.random.default_rng(621)
     wire = long_stream(rng, 32 << 20, mix3)
     cw = _cut_stream("garbage", rng, wire, keep_len=True)

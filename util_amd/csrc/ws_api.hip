@@ -33,7 +33,7 @@ extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
-extern WsOpt ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
+extern WsOpt ws_stream_split_capture, ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
     ws_stream_c1;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips,
@@ -117,6 +117,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_split2")) {
         if (value < 0 || value > 255) return -1;
         ws_stream_split2 = (int)value;
+    }
+    else if (!strcmp(name, "stream_split_capture")) {
+        if (value < 0 || value > 1) return -1;
+        ws_stream_split_capture = (int)value;
     }
     else if (!strcmp(name, "stream_c1")) {
         if (value < 0 || value > 6) return -1;

@@ -1410,6 +1410,9 @@ WsOpt ws_stream_split2{48};     // "stream_split2": a third part — K2's second
                                 // pieces (> stream_split; 0: two parts). Three parts 8 / 48 with part 0 in chunks of
                                 // C / 8 and the middle in C / 4: 7.53-7.56 ms against 7.57-7.59 for two parts 24 in
                                 // C / 4 (cfg3, profiles/r06_stream_split_ab.log)
+WsOpt ws_stream_split_capture{1};   // "stream_split_capture": split captured calls too (their side stream
+                                    // becomes a graph branch, run beside the unmask: cfg3 replays 7.60 ms
+                                    // against 7.84 unsplit, profiles/r06_stream_split_ab.log ab_gcap)
 WsOpt ws_stream_c1{2};          // "stream_c1": a middle part's chunks are the last part's chunk >> this
 WsOpt ws_stream_c0{3};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
@@ -1638,8 +1641,8 @@ static RwDevLayout rw_dev_layout(u64 len) {
 // The split of a device-planned walk (round 6): K2 runs as one launch per
 // part (pieces [0, p[0]), [p[0], p[1]), ..., [p[last], npieces)), and the walk of each part after
 // part 0 runs on a side stream while the earlier launches stream. Side-stream work joins the
-// caller's stream through events (a capture would fork and join through them too; captured calls
-// do not split, see the entry point).
+// caller's stream through events (a capture forks and joins through them too: the side stream's
+// work becomes a graph branch, option stream_split_capture).
 struct RwSplit {
     u32 ncut = 0;                // K2 cut points (parts - 1); 0 = no split
     u64 p[RW_NP - 1] = {};       // the cuts (pieces)
@@ -1852,9 +1855,9 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     RwSplit SP;
     unsigned char* const rw_w = reinterpret_cast<unsigned char*>(A.d) + WS_AUX_HEAD;
     const RwPlan* const rw_plan = reinterpret_cast<const RwPlan*>(rw_w + RL.o_plan);
-    // (eager calls only: a captured graph's branches are not run concurrently — the split measured
-    // 8.57-8.59 ms against 8.06-8.08 unsplit for cfg3 replays, profiles/r06_stream_split_ab.log)
-    if (dev_layout && !capture) {
+    // (captured calls too unless stream_split_capture is 0: the side stream's work becomes a graph
+    // branch, which the runtime runs beside the unmask's launches)
+    if (dev_layout && (!capture || ws_stream_split_capture)) {
         const int spl = ws_stream_split, spl2 = ws_stream_split2, sw = ws_stream_split_wait;   // one read each
         const int c0 = ws_stream_c0, c1 = ws_stream_c1, pr = ws_stream_side_prio;
         if (spl > 0 && spl < 256 && Pw.npieces >= 3) {
