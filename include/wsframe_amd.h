@@ -233,8 +233,9 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * frames of one length <= 16 KiB, / 6 for longer ones, and without advice / 7 for batches with
  * at least one segment per 8 pieces of 16 KiB, else / 6), "piece_win" (0..6: log2 of the windows the
  * unmask kernel streams side by side; -1 default: 2 for batches of >= 32 GiB, and of >= 16 GiB that the
- * previous call on the stream advised as frames of one length, else 1), "seg_win" (0/1: two windows for the
- * segment kernels), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
+ * previous call on the stream advised as frames of one length, else 1), "seg_win" (0..3: log2 of the windows
+ * the segment kernels stream side by side; -1 default: 4 windows for the segment decode, 8 for the
+ * fused reassembly; fewer below 256 segments per window), "reasm_path" (0 auto, 1 fused, 2 three-kernel), "reasm_cfg" (0..2: the
  * fused kernel's window/occupancy), "enc_front" (encode: 1 tile-scan front with the edge
  * chunks before the copy, 0 hipcub scan and an edge kernel after it), "host_chunk_mb",
  * "stream_rw" / "stream_rw_cmax" / "stream_rounds" / "stream_plink" (raw stream:

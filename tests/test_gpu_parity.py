@@ -352,10 +352,11 @@ def test_int_truncation_real_size(dev, decode_path, total):
 
 
 @pytest.mark.parametrize("opt,val", [("piece_win", 0), ("piece_win", 2), ("piece_win", 3), ("seg_win", 0),
-                                     ("piece_lds", 1), ("piece_lds", 56000)])
+                                     ("seg_win", 1), ("seg_win", 3), ("piece_lds", 1), ("piece_lds", 56000)])
 def test_window_mappings(dev, decode_path, opt, val):
     """K2's piece windows (piece_win = log2 W; the grid rounds up to W * ceil(P / W), spare
-    blocks store nothing), the segment kernels' two-window order (seg_win) and K2's
+    blocks store nothing), the segment kernels' 1 / 2 / 8-window orders (seg_win; the default is
+    4 / 8; 2101 segments: the last window's spare blocks) and K2's
     blocks-per-CU cap (piece_lds: 8 and 2 blocks instead of the default 5) at every setting,
     on a batch large enough for every window to be used: bit-exact vs the oracle"""
     W.set_option(opt, val)
@@ -365,13 +366,13 @@ def test_window_mappings(dev, decode_path, opt, val):
         so = [int(off[i]) for i in range(0, 2100, 16)]
         ends = so[1:] + [len(wire)]
         assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d" % (opt, val))
-        wire, off, pl, plain = wsynth.make_batch(16 * 1100, 0, 1024, 2, 78)   # cfg5 shape (segfuse)
-        so = [int(off[i]) for i in range(0, 16 * 1100, 16)]
+        wire, off, pl, plain = wsynth.make_batch(16 * 2101, 0, 1024, 2, 78)   # cfg5 shape (segfuse)
+        so = [int(off[i]) for i in range(0, 16 * 2101, 16)]
         ends = so[1:] + [len(wire)]
         assert_same(dev, wire, so, [e - s for s, e in zip(so, ends)], 16, tag="%s=%d cfg5" % (opt, val))
     finally:
         W.set_option("piece_win", -1)
-        W.set_option("seg_win", 1)
+        W.set_option("seg_win", -1)
         W.set_option("piece_lds", 0)
 
 

@@ -138,6 +138,21 @@ def test_reassemble_cfg5_shape(dev):
     assert all(len(m) == 1 and m[0][4] == 1 and m[0][1] == 16 * 1024 for m in oms)
 
 
+@pytest.mark.parametrize("swin", [-1, 0, 1, 2])
+def test_reassemble_segment_windows(dev, reasm_path, swin):
+    """the fused kernel's segment windows (seg_win: 2^k windows streamed side by side, -1 the
+    default 8) over 2,101 cfg5-shaped segments — the last window's spare blocks store nothing"""
+    if reasm_path != 1:
+        pytest.skip("fused kernel option")
+    W.set_option("seg_win", swin)
+    try:
+        wl = bench.Workload.make("cfg5", dev, nframes=16 * 2101)
+        wire = wl.buf[:wl.wire_bytes].cpu().numpy().copy()
+        check(dev, wire, wl.seg_off_h, wl.seg_len_h, 16, tag="seg_win %d" % swin)
+    finally:
+        W.set_option("seg_win", -1)
+
+
 def _frame(rng, plen, masked=True, b0=0x82, form=None):
     key = rng.integers(0, 256, 4, dtype=np.uint8) if masked else None
     form = form or (7 if plen < 126 else (16 if plen <= 0xFFFF else 64))

@@ -19,7 +19,7 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 wins = [int(x) for x in os.environ.get("EXP_WIN", "1,2").split(",")]
 opt = os.environ.get("EXP_OPT", "piece_win")                  # seg_win: the segment kernels (cfg5)
-dflt = {"piece_win": -1, "seg_win": 1, "piece_dir": 0}.get(opt, 0)
+dflt = {"piece_win": -1, "seg_win": -1, "piece_dir": 0}.get(opt, 0)
 dev = torch.device("cuda", 0)
 wls = [bench.Workload.make(cfg, dev) for _ in range(K)]
 torch.cuda.synchronize()

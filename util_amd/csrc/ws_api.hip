@@ -31,7 +31,8 @@ void ws_k2_timing_reset();
 int ws_k2_stat(unsigned long long* ns, unsigned long long* calls);
 extern WsOpt ws_enc_front;
 extern WsOpt ws_scan_alpha;
-WsOpt ws_seg_win{1};      // "seg_win": segfuse and fused reassembly take segments in two windows (ws_win2)
+WsOpt ws_seg_win{-1};     // "seg_win": segfuse and fused reassembly take segments in 2^seg_win windows (ws_winn);
+                          // -1: 4 windows for segfuse, 8 for the fused reassembly (profiles/r06_seg_win_ab.log)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
 extern WsOpt ws_stream_split_capture, ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
     ws_stream_c1;
@@ -79,7 +80,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
         ws_piece_win = (int)value;
     }
     else if (!strcmp(name, "seg_win")) {
-        if (value < 0 || value > 1) return -1;
+        if (value < -1 || value > 3) return -1;
         ws_seg_win = (int)value;
     }
     else if (!strcmp(name, "reasm_path")) {

@@ -470,7 +470,7 @@ __global__ __launch_bounds__(256) void ws_calib_windows_dep_kernel(gu32x4* __res
 
 // modes 73-75: the segment-kernel shape (segfuse / fused reassembly) without frame logic:
 // one 256-thread block per "segment" of `segc` 16-B chunks (cfg5: 1032), segments taken in
-// two windows (ws_win2), in-place XOR. 73: LDS-DMA of the segment (1 KiB slices by every
+// two windows (ws_winn), in-place XOR. 73: LDS-DMA of the segment (1 KiB slices by every
 // wave), barrier, XOR from LDS, store (segfuse's data path); 74: the segment in registers
 // (U chunks per lane), XOR, store (K2's data path at segment granularity); 75: as 74 plus a
 // copy of the registers into LDS and a barrier before the stores (what a register-resident

@@ -446,8 +446,18 @@ size_t ws_decode_workspace_bytes(u64 span, u32 nseg, u32 max_frames);
 int ws_launch_segfuse(const WsLaunch& L);
 bool ws_segfuse_fits(u64 span, u32 nseg, u32 max_frames);
 
-// Block -> work item with the items split into two windows streamed side by side
-// (block b takes item (b & 1) * half + b / 2; half = 0 keeps b): two distant address
+// Block -> work item with the items split into 2^wsh windows of ppw items streamed side by side
+// (block b takes item (b mod 2^wsh) * ppw + b / 2^wsh; wsh = 0 keeps b): two distant address
 // windows in flight beat one compact window on this HBM (tools/exp_win.sh).
-__device__ __forceinline__ u32 ws_win2(u32 b, u32 half) { return half ? (b & 1u) * half + (b >> 1) : b; }
+__device__ __forceinline__ u32 ws_winn(u32 b, u32 wsh, u32 ppw) {
+    return wsh ? (b & ((1u << wsh) - 1u)) * ppw + (b >> wsh) : b;
+}
+// the grid of ws_winn for n items in 2^wsh windows (fewer windows for small n): {wsh, ppw, blocks}
+struct WsWinGrid { u32 wsh, ppw, blocks; };
+static inline WsWinGrid ws_win_grid(u32 n, int opt) {
+    u32 wsh = opt > 0 && opt <= 3 ? (u32)opt : 0u;
+    while (wsh && (n >> wsh) < 256) --wsh;                 // (two windows from 512 items, as before)
+    const u32 ppw = wsh ? (u32)(((u64)n + (1u << wsh) - 1) >> wsh) : n;
+    return WsWinGrid{wsh, ppw, wsh ? ppw << wsh : n};
+}
 extern WsOpt ws_seg_win;

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     const unsigned char* __restrict__ buf, u32 max_frames, const u64* __restrict__ seg_off,
     const u64* __restrict__ seg_len, WebsocketFrameDesc_t* __restrict__ desc, WebsocketSegResult_t* __restrict__ res,
     unsigned char* __restrict__ out, const u64* __restrict__ out_off, WebsocketMsgDesc_t* __restrict__ msg,
-    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io, u32 merge, u32 nseg, u32 half, u32 cache_max,
+    u32* __restrict__ nmsg, unsigned char* __restrict__ open_io, u32 merge, u32 nseg, u32 wsh, u32 ppw, u32 cache_max,
     u32* __restrict__ cached_io) {
     constexpr u32 RSEG_C = (RSEG_L - 1) * 64;         // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[RSEG_L * 64];
@@ -313,8 +313,8 @@ __global__ __launch_bounds__(RSEG_T) __attribute__((amdgpu_waves_per_eu(MINW, 8)
     __shared__ u32 tkey[RSEG_TB];
     __shared__ u64 sh_next;                        // next window's first chunk, ~0 = done
     __shared__ u32 sh_blo, sh_bhi;                 // bodies with bytes in this window [blo, bhi], blo > bhi: none
-    const u32 s = ws_win2(blockIdx.x, half), tid = threadIdx.x, lane = tid & 63;
-    if (s >= nseg) return;                         // the odd grid's spare block
+    const u32 s = ws_winn(blockIdx.x, wsh, ppw), tid = threadIdx.x, lane = tid & 63;
+    if (s >= nseg) return;                         // the last window's spare blocks
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool w0 = wv == 0;
     const u64 so = seg_off[s], sl = seg_len[s];
@@ -563,11 +563,12 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeBatchReassembleDeviceEx(
     const bool fused = rpath == 1 || (rpath == 0 && max_frames <= RSEG_TB && nseg >= 1024 && buflen <= (u64)nseg << 18);
     if (fused && max_frames <= RSEG_TB) {
         auto k = rcfg == 1 ? ws_reasm_seg_kernel<18, 1> : (rcfg == 2 ? ws_reasm_seg_kernel<20, 1> : ws_reasm_seg_kernel<18, 8>);
-        const u32 half = ws_seg_win && nseg >= 512 ? (nseg + 1) / 2 : 0;
+        const int swin = ws_seg_win;                                   // one read per call
+        const WsWinGrid wg = ws_win_grid(nseg, swin < 0 ? 3 : swin);
         // (body-boundary chunks: one byte-store instruction from 31 lanes; one lane assembling
         // them whole measured slower, cfg5u 1.65 vs 1.50 ms)
-        hipLaunchKernelGGL(k, dim3(half ? 2 * half : nseg), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
-                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, 0u, nseg, half,
+        hipLaunchKernelGGL(k, dim3(wg.blocks), dim3(RSEG_T), 0, st, d_buf, max_frames, d_seg_off,
+                           d_seg_len, d_desc, d_res, d_out, d_out_off, d_msg, d_nmsg, d_open, 0u, nseg, wg.wsh, wg.ppw,
                            (u32)readcache_max_size, d_cached);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : ws_set_err("ws_reasm_seg_kernel launch", e);

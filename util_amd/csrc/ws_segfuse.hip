@@ -43,14 +43,14 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
                                                           const u64* __restrict__ seg_len, u32 max_frames,
                                                           const u64* __restrict__ desc_base,
                                                           WebsocketFrameDesc_t* __restrict__ desc,
-                                                          WebsocketSegResult_t* __restrict__ res, u32 nseg, u32 half) {
+                                                          WebsocketSegResult_t* __restrict__ res, u32 nseg, u32 wsh, u32 ppw) {
     constexpr u32 SF_C = (SF_L - 1) * 64;             // chunks owned per window
     __shared__ __attribute__((aligned(16))) u32x4 win[SF_L * 64];
     __shared__ FrameL tab[SF_TB];
     __shared__ u64 sh_next;                         // next window's first chunk, ~0 = done
     __shared__ u32 sh_flo, sh_fhi;                  // frames with bytes in this window [flo, fhi)
-    const u32 s = ws_win2(blockIdx.x, half), tid = threadIdx.x, lane = tid & 63;
-    if (s >= nseg) return;                          // the odd grid's spare block
+    const u32 s = ws_winn(blockIdx.x, wsh, ppw), tid = threadIdx.x, lane = tid & 63;
+    if (s >= nseg) return;                          // the last window's spare blocks
     const u32 wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const u64 so = seg_off[s], sl = seg_len[s];
     const uintptr_t segp = reinterpret_cast<uintptr_t>(buf + so);
@@ -164,9 +164,10 @@ __global__ __launch_bounds__(SF_T) void ws_segfuse_kernel(unsigned char* __restr
 // (5 per CU 20 % slower), plain (not nontemporal) loads and stores.
 int ws_launch_segfuse(const WsLaunch& L) {
     if (L.max_frames > SF_TB) return ws_set_msg("segfuse path: max_frames > 64");
-    const u32 half = ws_seg_win && L.nseg >= 512 ? (L.nseg + 1) / 2 : 0;
-    hipLaunchKernelGGL((ws_segfuse_kernel<4, 18, 256>), dim3(half ? 2 * half : L.nseg), dim3(256), 0, L.stream, L.buf,
-                       L.seg_off, L.seg_len, L.max_frames, L.desc_base, L.desc, L.res, L.nseg, half);
+    const int swin = ws_seg_win;                                         // one read per call
+    const WsWinGrid wg = ws_win_grid(L.nseg, swin < 0 ? 2 : swin);
+    hipLaunchKernelGGL((ws_segfuse_kernel<4, 18, 256>), dim3(wg.blocks), dim3(256), 0, L.stream, L.buf,
+                       L.seg_off, L.seg_len, L.max_frames, L.desc_base, L.desc, L.res, L.nseg, wg.wsh, wg.ppw);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : ws_set_err("ws_segfuse_kernel launch", e);
 }
