@@ -250,7 +250,8 @@ WSFRAME_AMD_EXPORT const char* websocketframeGpuLastError(void);
  * past "stream_split", default 48, 0 = two parts — a middle part, in chunks of that chunk >> "stream_c1"
  * (default 2); "stream_side_prio": the side stream's priority, 0
  * default (default), 1 least, 2 greatest); "stream_split_capture" (0/1, default 1: captured calls
- * split too, the side stream becoming a graph branch; 0 = captured calls take one launch), "k2_timing" (see
+ * split too, the side stream becoming a graph branch; 0 = captured calls take one launch), "stream_win" (-1..6: log2 of the piece windows of a raw-stream
+ * call's unmask launches, default 2 = four; -1 the batch rule of "piece_win"), "k2_timing" (see
  * websocketframeGpuGetStat). Options are atomics read once per call. Returns 0, or -1 for an
  * unknown name or a value out of range. */
 WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, long long value);

@@ -22,14 +22,14 @@ torch = pytest.importorskip("torch")
 DEFAULTS = {"path": -1, "scan_alpha": 1, "host_chunk_mb": 64, "piece_lds": 0,
             "piece_win": -1, "seg_win": -1, "reasm_path": 0, "reasm_cfg": 0, "enc_front": 1, "stream_rw": 1,
             "stream_rw_cmax": 22, "stream_rounds": 4, "stream_plink": 1, "stream_split": 8, "stream_split_wait": 0,
-            "stream_c0": 3, "stream_side_prio": 0, "stream_split2": 48, "stream_c1": 2, "stream_split_capture": 1, "k2_timing": 0}
+            "stream_c0": 3, "stream_side_prio": 0, "stream_split2": 48, "stream_c1": 2, "stream_split_capture": 1, "stream_win": 2, "k2_timing": 0}
 
 VALUES = {"path": [-1, 1, 3, 4], "scan_alpha": [0, 1],
           "host_chunk_mb": [1, 64], "piece_lds": [0, 1, 56000], "piece_win": [-1, 0, 1, 2, 3, 4, 5, 6],
           "seg_win": [-1, 0, 1, 2, 3], "reasm_path": [0, 1, 2], "reasm_cfg": [0, 1, 2], "enc_front": [0, 1],
           "stream_rw": [0, 1, 2], "stream_rw_cmax": [16, 20, 23, 26], "stream_rounds": [1, 4, 64], "stream_plink": [0, 1],
           "stream_split": [0, 1, 16, 128, 255], "stream_split_wait": [0, 1, 2], "stream_c0": [0, 2, 6],
-          "stream_side_prio": [0, 1, 2], "stream_split2": [0, 64, 200], "stream_c1": [0, 1, 3], "stream_split_capture": [0, 1],
+          "stream_side_prio": [0, 1, 2], "stream_split2": [0, 64, 200], "stream_c1": [0, 1, 3], "stream_split_capture": [0, 1], "stream_win": [-1, 0, 1, 3],
           "k2_timing": [0, 1]}
 
 # options that act only inside the piece path: the case runs it
@@ -105,6 +105,6 @@ def test_out_of_range_values_refused():
                      ("reasm_path", 3), ("reasm_cfg", 3), ("enc_front", 2), ("stream_rw_cmax", 27),
                      ("stream_rounds", 0), ("host_chunk_mb", 0), ("piece_lds", -1),
                      ("stream_split", 256), ("stream_split_wait", 3), ("stream_c0", 7), ("stream_split2", 256),
-                     ("stream_c1", 7), ("stream_split_capture", 2)]:
+                     ("stream_c1", 7), ("stream_split_capture", 2), ("stream_win", 7), ("stream_win", -2)]:
         with pytest.raises(ValueError):
             W.set_option(opt, bad)

@@ -34,7 +34,7 @@ extern WsOpt ws_scan_alpha;
 WsOpt ws_seg_win{-1};     // "seg_win": segfuse and fused reassembly take segments in 2^seg_win windows (ws_winn);
                           // -1: 4 windows for segfuse, 8 for the fused reassembly (profiles/r06_seg_win_ab.log)
 extern WsOpt ws_stream_rw, ws_stream_rw_cmax, ws_stream_rounds, ws_stream_plink;
-extern WsOpt ws_stream_split_capture, ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
+extern WsOpt ws_stream_win, ws_stream_split_capture, ws_stream_split, ws_stream_split_wait, ws_stream_c0, ws_stream_side_prio, ws_stream_split2,
     ws_stream_c1;
 size_t ws_workspace_bytes_total();
 extern std::atomic<unsigned long long> ws_stat_rw_chunks, ws_stat_rw_chunk_walks, ws_stat_stream_skips,
@@ -118,6 +118,10 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeGpuSetOption(const char* name, l
     else if (!strcmp(name, "stream_split2")) {
         if (value < 0 || value > 255) return -1;
         ws_stream_split2 = (int)value;
+    }
+    else if (!strcmp(name, "stream_win")) {
+        if (value < -1 || value > 6) return -1;
+        ws_stream_win = (int)value;
     }
     else if (!strcmp(name, "stream_split_capture")) {
         if (value < 0 || value > 1) return -1;

@@ -381,6 +381,7 @@ struct WsLaunch {
     hipStream_t stream;
     int cus;
     int lds_per_cu;       // bytes of LDS per CU (hipDeviceProp_t::maxSharedMemoryPerMultiProcessor)
+    int pwin = -1;        // K2's log2 piece windows for this call (-1: the batch rule, piece_wshift)
 };
 int ws_launch_walker(const WsLaunch& L, const u32* gate = nullptr, u32 gate_gen = 0);
 size_t ws_piece_workspace_bytes(u64 span, u32 nseg, u32 max_frames);

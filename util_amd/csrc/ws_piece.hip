@@ -694,8 +694,9 @@ int ws_k2_mark(hipStream_t st, bool end, size_t* slot) {
 // four windows whatever the advice, 1-2 M pieces four only when advised as one frame length.
 #define PIECE_WIN4_MIN (1ull << 20)
 #define PIECE_WIN4_BIG (2ull << 20)
-static u32 piece_wshift(u64 npieces, u32 g0) {
+static u32 piece_wshift(u64 npieces, u32 g0, int call_win) {
     int pwin = ws_piece_win;
+    if (pwin < 0 && call_win >= 0) pwin = call_win;                      // the caller's choice (raw stream)
     if (pwin < 0) pwin = npieces >= PIECE_WIN4_BIG || (g0 >= 2 && npieces >= PIECE_WIN4_MIN) ? 2 : 1;
     u32 wshift = (u32)(pwin > 6 ? 6 : pwin);
     while (wshift && (npieces >> wshift) < 256) --wshift;                // small batches: one window
@@ -711,7 +712,7 @@ int ws_launch_piece_unmask(const WsLaunch& L, const PieceWs& P, u32 gen, int* ad
     int rc;
     const int timing = ws_k2_timing;
     if (timing && (rc = ws_k2_mark(L.stream, false, &tslot))) return rc;
-    const u32 wshift = piece_wshift(P.npieces, g0);
+    const u32 wshift = piece_wshift(P.npieces, g0, L.pwin);
     ws_stat_k2_windows = 1ull << wshift;
     const u64 ppw = (P.npieces + (1ull << wshift) - 1) >> wshift;
     const u64 grid = ppw << wshift;

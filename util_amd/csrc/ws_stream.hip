@@ -1413,6 +1413,9 @@ WsOpt ws_stream_split2{48};     // "stream_split2": a third part — K2's second
 WsOpt ws_stream_split_capture{1};   // "stream_split_capture": split captured calls too (their side stream
                                     // becomes a graph branch, run beside the unmask: cfg3 replays 7.60 ms
                                     // against 7.84 unsplit, profiles/r06_stream_split_ab.log ab_gcap)
+WsOpt ws_stream_win{2};         // "stream_win": log2 of the piece windows of a raw-stream call's unmask launches
+                                // (-1: the batch rule); four windows: cfg3 7.41 against 7.54 ms with two
+                                // (profiles/r06_stream_win_ab.log)
 WsOpt ws_stream_c1{2};          // "stream_c1": a middle part's chunks are the last part's chunk >> this
 WsOpt ws_stream_c0{3};          // "stream_c0": part 0's chunks are the usual chunk >> this (at least twice its window)
 std::atomic<unsigned long long> ws_stat_rw_chunks{0};       // chunks written from records (last call)
@@ -1810,6 +1813,7 @@ extern "C" WSFRAME_AMD_EXPORT int websocketframeStreamDecodeDevice(unsigned char
     L.buf = d_buf; L.seg_off = d_seg; L.seg_len = d_seg + 1; L.nseg = 1; L.max_frames = max_frames;
     L.desc_base = nullptr; L.desc = d_desc; L.res = d_res; L.stream = st;
     L.cus = slot.cus; L.lds_per_cu = slot.lds;
+    L.pwin = ws_stream_win;
     PieceWs Pw;
     const u32 gen = ws_next_gen();
     // the piece-path views of the workspace
